@@ -1,0 +1,159 @@
+"""ctypes mirror of ``include/flacmi.h`` (the C-ABI of libflacmi.so).
+
+Kept in one place so the product loader (``_lib.py``) and the test harness agree on
+struct layouts.  Pure data definitions: importing this module loads no library.
+"""
+import ctypes as C
+
+import numpy as np
+
+ABI_VERSION = 1
+MAX_LPC_ORDER = 32
+MAX_BLOCK = 32768
+MAX_RICE_ORDER = 15
+STATS_WORDS = 128
+
+
+def lpc_rec_words(L: int) -> int:
+    return 2 + L + (L * (L + 1)) // 2
+
+
+# flacmi_status
+STATUS_OK = 0
+STATUS_ZERO_DIVISION = 1
+STATUS_ASSERTION = 2
+STATUS_VALUE_ERROR = 3
+STATUS_OVERFLOW = 4
+STATUS_RESIDUAL_WIDE = 16
+
+STATUS_EXCEPTION = {
+    STATUS_ZERO_DIVISION: ZeroDivisionError,
+    STATUS_ASSERTION: AssertionError,
+    STATUS_VALUE_ERROR: ValueError,
+    STATUS_OVERFLOW: OverflowError,
+}
+
+# flacmi_site
+SITE_NAMES = {
+    0: "none",
+    1: "tukey: float division by zero (encoder.py:437)",
+    2: "levinson_durbin: float division by zero (encoder.py:469)",
+    3: "levinson_durbin: lambda_ ** 2 overflow (encoder.py:476)",
+    4: "quantize_lpc_coefficients: assert coef_max > 0.0 (encoder.py:496)",
+    5: "quantize_lpc_coefficients: floor(log2(inf)) (encoder.py:503)",
+    6: "quantize_lpc_coefficients: shift < shift_min (encoder.py:508)",
+    7: "quantize_lpc_coefficients: round(inf) (encoder.py:520)",
+    8: "quantize_lpc_coefficients: round(nan) (encoder.py:520)",
+    9: "encode_subframe_lpc: min() arg is an empty sequence (encoder.py:404)",
+    10: "encode: fixed and LPC residual sums tie (encoder.py:157)",
+    11: "rice_partitions: no valid partition order (encoder.py:669)",
+    12: "find_rice_parameter: math domain error (encoder.py:753)",
+    13: "rice_size: negative shift count (encoder.py:758)",
+    14: "residual does not fit the requested element width",
+}
+
+MODE_REFERENCE = 0
+MODE_FIXED_ONLY = 1
+KIND_FIXED = 0
+KIND_LPC = 1
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("max_lpc_order", C.c_int32),
+        ("qlp_precision", C.c_int32),
+        ("rice_min", C.c_int32),
+        ("rice_max", C.c_int32),
+        ("mode", C.c_int32),
+        ("reserved", C.c_int32 * 3),
+    ]
+
+
+class Batch(C.Structure):
+    _fields_ = [
+        ("samples", C.c_void_p),
+        ("sample_bytes", C.c_int32),
+        ("sample_bits", C.c_int32),
+        ("unit_stride", C.c_int64),
+        ("n_units", C.c_int64),
+        ("block_len", C.c_int32),
+        ("tail_len", C.c_int32),
+        ("n_tail_units", C.c_int64),
+    ]
+
+
+class UnitMeta(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("site", C.c_int32),
+        ("kind", C.c_int32),
+        ("order", C.c_int32),
+        ("shift", C.c_int32),
+        ("ncoefs", C.c_int32),
+        ("res_offset", C.c_int32),
+        ("res_len", C.c_int32),
+        ("fixed_order", C.c_int32),
+        ("lpc_order", C.c_int32),
+        ("part_order", C.c_int32),
+        ("n_parts", C.c_int32),
+        ("coding_method", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("fixed_sum", C.c_int64),
+        ("lpc_sum", C.c_int64),
+        ("rice_bits", C.c_int64),
+        ("coefs", C.c_int32 * MAX_LPC_ORDER),
+    ]
+
+
+# numpy view of flacmi_unit_meta, for zero-copy access to a meta array
+META_DTYPE = np.dtype([
+    ("status", "<i4"), ("site", "<i4"), ("kind", "<i4"), ("order", "<i4"),
+    ("shift", "<i4"), ("ncoefs", "<i4"), ("res_offset", "<i4"), ("res_len", "<i4"),
+    ("fixed_order", "<i4"), ("lpc_order", "<i4"), ("part_order", "<i4"), ("n_parts", "<i4"),
+    ("coding_method", "<i4"), ("reserved0", "<i4"),
+    ("fixed_sum", "<i8"), ("lpc_sum", "<i8"), ("rice_bits", "<i8"),
+    ("coefs", "<i4", (MAX_LPC_ORDER,)),
+])
+assert META_DTYPE.itemsize == C.sizeof(UnitMeta) == 208
+
+
+class Outputs(C.Structure):
+    _fields_ = [
+        ("meta", C.c_void_p),
+        ("rice_params", C.c_void_p),
+        ("params_stride", C.c_int64),
+        ("residual", C.c_void_p),
+        ("residual_bytes", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("residual_stride", C.c_int64),
+        ("acf", C.c_void_p),
+        ("fixed_sums", C.c_void_p),
+        ("lpc_sums", C.c_void_p),
+        ("lpc_records", C.c_void_p),
+    ]
+
+
+# Every symbol include/flacmi.h declares, with its ctypes signature.
+SIGNATURES = {
+    "flacmi_abi_version": (C.c_int, []),
+    "flacmi_last_error": (C.c_char_p, []),
+    "flacmi_device_count": (C.c_int, []),
+    "flacmi_create": (C.c_void_p, [C.c_int]),
+    "flacmi_destroy": (None, [C.c_void_p]),
+    "flacmi_analyze_device": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Params),
+                                        C.POINTER(Outputs), C.c_void_p]),
+    "flacmi_analyze_host": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Params),
+                                      C.POINTER(Outputs)]),
+    "flacmi_stream_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
+                                      C.c_int64, C.c_void_p, C.c_void_p]),
+    "flacmi_synth_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,
+                                      C.c_int64, C.c_int64, C.c_int32, C.c_uint64, C.c_void_p]),
+    "flacmi_device_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),
+    "flacmi_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "flacmi_memcpy_h2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "flacmi_memcpy_d2h": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "flacmi_synchronize": (C.c_int, [C.c_void_p]),
+    "flacmi_last_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int]),
+    "flacmi_host_pypow2": (C.c_double, [C.c_double, C.POINTER(C.c_int32)]),
+    "flacmi_host_floor_log2": (C.c_int32, [C.c_double]),
+}

@@ -1,0 +1,219 @@
+/*
+ * flacmi.h — C-ABI of the MI355X FLAC encode-analysis library (libflacmi.so).
+ *
+ * This is the drop-in boundary for turlando/flac-py's per-block analysis hot path.
+ * flac-py has no FFI layer of its own; the interface this library replaces is the
+ * Python function triple called once per (block, channel) from encode():
+ *
+ *   encode_subframe_fixed(samples)                       flac/encoder.py:331-359
+ *   encode_subframe_lpc(samples, lpc_order, precision)   flac/encoder.py:362-420
+ *     (tukey 423-440, autocorrelation 443-450, levinson_durbin 453-479,
+ *      quantize_lpc_coefficients 482-534, prediction_residual 537-548)
+ *   the fixed-vs-LPC choice on sum(|residual|)           flac/encoder.py:133-157
+ *   encode_residual(residual, block_size, sample_size,
+ *                   predictor_order, partition_order_range)  flac/encoder.py:632-760
+ *     (called by the writer at flac/encoder.py:588 and :608)
+ *
+ * One call analyses a whole batch of independent "units" (one unit = one channel of
+ * one block) and returns, per unit, exactly the fields of the reference's
+ * SubframeHeader / SubframeFixed / SubframeLPC / Residual / RicePartition values
+ * (flac/common.py:286-309, 334-361, 378-420), bit-identical.  Where the reference
+ * would raise a Python exception the unit's `status` names the exception class and
+ * `site` names the raising statement (see flacmi_status / flacmi_site).
+ *
+ * Conventions: plain C types, caller-owned buffers, return 0 on success or a
+ * negative flacmi_error; flacmi_last_error() describes the last failure of the
+ * calling thread.  A context is bound to one HIP device and is not thread-safe;
+ * use one context per host thread.  The *_device entry points take device pointers
+ * and enqueue on the given hipStream_t (passed as void*), returning without a host
+ * synchronisation; the *_host entry points take host pointers and are synchronous.
+ */
+#ifndef FLACMI_H
+#define FLACMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLACMI_ABI_VERSION 1
+#define FLACMI_MAX_LPC_ORDER 32      /* EncoderParameters: lpc_order.stop <= 33 (encoder.py:42) */
+#define FLACMI_MAX_BLOCK 32768       /* largest block size flac-py encodes (common.py BLOCK_SIZE_ENCODING) */
+#define FLACMI_MAX_RICE_ORDER 15     /* 4-bit partition-order field (encoder.py:767) */
+#define FLACMI_LPC_REC_WORDS(L) (2 + (L) + ((L) * ((L) + 1)) / 2)
+
+/* ---- return codes (API level) ------------------------------------------------ */
+enum flacmi_error {
+    FLACMI_OK = 0,
+    FLACMI_E_INVALID = -1,       /* bad argument (shape, range, alignment) */
+    FLACMI_E_HIP = -2,           /* HIP runtime error */
+    FLACMI_E_UNSUPPORTED = -3,   /* shape this build does not handle (see flacmi_last_error) */
+    FLACMI_E_NOMEM = -4,
+};
+
+/* ---- per-unit status: the Python exception the reference would raise ---------- */
+enum flacmi_status {
+    FLACMI_STATUS_OK = 0,
+    FLACMI_STATUS_ZERO_DIVISION = 1,  /* ZeroDivisionError */
+    FLACMI_STATUS_ASSERTION = 2,      /* AssertionError */
+    FLACMI_STATUS_VALUE_ERROR = 3,    /* ValueError */
+    FLACMI_STATUS_OVERFLOW = 4,       /* OverflowError */
+    FLACMI_STATUS_RESIDUAL_WIDE = 16, /* not a reference exception: chosen residual does not fit
+                                         the requested residual element width; re-run with 8 bytes */
+};
+
+/* ---- per-unit site: which reference statement raises ------------------------------ */
+enum flacmi_site {
+    FLACMI_SITE_NONE = 0,
+    FLACMI_SITE_TUKEY = 1,           /* encoder.py:437  pi*i/nr with nr == 0 (4 <= n <= 7) */
+    FLACMI_SITE_LEVINSON_DIV = 2,    /* encoder.py:469  lambda_ /= error, error == 0 */
+    FLACMI_SITE_LEVINSON_POW = 3,    /* encoder.py:476  lambda_ ** 2 overflows */
+    FLACMI_SITE_QUANT_CMAX = 4,      /* encoder.py:496  assert coef_max > 0.0 */
+    FLACMI_SITE_QUANT_LOG2 = 5,      /* encoder.py:503  floor(log2(inf)) */
+    FLACMI_SITE_QUANT_SHIFT = 6,     /* encoder.py:508  shift < shift_min */
+    FLACMI_SITE_QUANT_ROUND_INF = 7, /* encoder.py:520/530 round(inf) */
+    FLACMI_SITE_QUANT_ROUND_NAN = 8, /* encoder.py:520/530 round(nan) */
+    FLACMI_SITE_LPC_EMPTY = 9,       /* encoder.py:404  min() of no candidate orders (-l 0) */
+    FLACMI_SITE_CHOICE_TIE = 10,     /* encoder.py:157  fixed_size == lpc_size */
+    FLACMI_SITE_RICE_NO_ORDER = 11,  /* encoder.py:669  no valid partition order */
+    FLACMI_SITE_RICE_LOG_DOMAIN = 12,/* encoder.py:753  log2(0): partition sum is 0 */
+    FLACMI_SITE_RICE_NEG_SHIFT = 13, /* encoder.py:758  1 << parameter, parameter < 0 */
+    FLACMI_SITE_RESIDUAL_WIDTH = 14, /* not a reference site: see FLACMI_STATUS_RESIDUAL_WIDE */
+};
+
+/* ---- analysis modes -------------------------------------------------------------- */
+enum flacmi_mode {
+    FLACMI_MODE_REFERENCE = 0,   /* fixed + LPC + choice + Rice, exactly as encode() does */
+    FLACMI_MODE_FIXED_ONLY = 1,  /* fixed predictor + Rice only (BASELINE config 5; the
+                                    reference's own -l 0 raises ValueError instead) */
+};
+
+enum flacmi_kind { FLACMI_KIND_FIXED = 0, FLACMI_KIND_LPC = 1 };
+
+typedef struct flacmi_params {
+    int32_t max_lpc_order;   /* L = lpc_order.stop - 1, 0..32 (lpc_order.start must be 0) */
+    int32_t qlp_precision;   /* EncoderParameters.qlp_precision, 5..31 */
+    int32_t rice_min;        /* rice_partition_order.start */
+    int32_t rice_max;        /* rice_partition_order.stop - 1 (rice_max < rice_min: empty range) */
+    int32_t mode;            /* flacmi_mode */
+    int32_t reserved[3];
+} flacmi_params;
+
+/* One batch of units.  Samples are planar: unit u occupies
+ * samples[u*unit_stride .. u*unit_stride + len(u)).  Every unit has `block_len`
+ * samples except the last `n_tail_units`, which have `tail_len` (the short last
+ * block of a stream, one unit per channel).  Rows must be 16-byte aligned. */
+typedef struct flacmi_batch {
+    const void* samples;     /* int16 (sample_bytes 2) or int32 (sample_bytes 4) */
+    int32_t sample_bytes;    /* 2 or 4 */
+    int32_t sample_bits;     /* every sample fits a signed integer of this many bits (<= 8*sample_bytes) */
+    int64_t unit_stride;     /* elements between consecutive units */
+    int64_t n_units;
+    int32_t block_len;       /* 1..FLACMI_MAX_BLOCK */
+    int32_t tail_len;        /* length of the trailing units, 1..block_len (ignored if n_tail_units == 0) */
+    int64_t n_tail_units;    /* 0..n_units */
+} flacmi_batch;
+
+/* Per-unit result.  Field names follow flac/common.py:
+ *   kind/order        -> SubframeHeader.type_ = SubframeTypeFixed(order) | SubframeTypeLPC(order)
+ *   warmup            -> samples[:order]  (not copied: the caller has the samples)
+ *   shift/coefs/ncoefs-> SubframeLPC.shift / .coefficients (qlp precision is the parameter)
+ *   residual          -> residual row [res_offset, res_offset + res_len), zig-zag encoded,
+ *                        i.e. the concatenation of RicePartition.residual
+ *   part_order/n_parts/coding_method/rice params -> Residual  */
+typedef struct flacmi_unit_meta {
+    int32_t status;          /* flacmi_status */
+    int32_t site;            /* flacmi_site */
+    int32_t kind;            /* flacmi_kind of the chosen subframe */
+    int32_t order;           /* predictor order of the chosen subframe = len(warmup) */
+    int32_t shift;           /* SubframeLPC.shift (0 for fixed) */
+    int32_t ncoefs;          /* len(SubframeLPC.coefficients): order, or 0 in the negative-shift branch */
+    int32_t res_offset;      /* first valid element of the residual row */
+    int32_t res_len;         /* len(residual) */
+    int32_t fixed_order;     /* best fixed order 0..4 */
+    int32_t lpc_order;       /* best LPC order 1..L (0 in fixed-only mode) */
+    int32_t part_order;      /* Residual.partition_order as chosen by rice_partitions */
+    int32_t n_parts;         /* len(Residual.partitions) */
+    int32_t coding_method;   /* RiceCodingMethod value: 4 or 5 */
+    int32_t reserved0;
+    int64_t fixed_sum;       /* sum(|r|) of the best fixed residual */
+    int64_t lpc_sum;         /* sum(|r|) of the best LPC residual (0 in fixed-only mode) */
+    int64_t rice_bits;       /* size estimate of the chosen partitioning (encoder.py:714-727) */
+    int32_t coefs[FLACMI_MAX_LPC_ORDER];
+} flacmi_unit_meta;
+
+typedef struct flacmi_outputs {
+    flacmi_unit_meta* meta;  /* [n_units] */
+    int32_t* rice_params;    /* [n_units][params_stride], RicePartition.parameter per partition */
+    int64_t params_stride;   /* >= 2^rice_max + 1 */
+    void* residual;          /* [n_units][residual_stride] uint32 or uint64 zig-zag residuals */
+    int32_t residual_bytes;  /* 4 or 8 */
+    int32_t reserved0;
+    int64_t residual_stride; /* elements, >= block_len */
+    /* optional intermediates (NULL to skip), used by parity tests */
+    double* acf;             /* [n_units][33]  autocorrelation lags 0..L */
+    int64_t* fixed_sums;     /* [n_units][5]   sum(|r|) for fixed orders 0..4 */
+    int64_t* lpc_sums;       /* [n_units][32]  sum(|r|) for LPC orders 1..L */
+    int32_t* lpc_records;    /* [n_units][FLACMI_LPC_REC_WORDS(32)] status/site, negmask, shifts, coefs */
+} flacmi_outputs;
+
+typedef struct flacmi_ctx flacmi_ctx;
+
+/* ---- library / context ------------------------------------------------------------ */
+int flacmi_abi_version(void);
+const char* flacmi_last_error(void);
+int flacmi_device_count(void);
+flacmi_ctx* flacmi_create(int device);
+void flacmi_destroy(flacmi_ctx* ctx);
+
+/* ---- the hot path ---------------------------------------------------------------- */
+/* Device pointers, enqueued on `stream` (hipStream_t). */
+int flacmi_analyze_device(flacmi_ctx* ctx, const flacmi_batch* batch,
+                          const flacmi_params* params, const flacmi_outputs* out,
+                          void* stream);
+/* Host pointers; copies in and out, synchronous. */
+int flacmi_analyze_host(flacmi_ctx* ctx, const flacmi_batch* batch,
+                        const flacmi_params* params, const flacmi_outputs* out);
+
+/* ---- stream statistics (reduced across GPUs with one RCCL all-reduce) ------------- */
+#define FLACMI_STATS_WORDS 128
+/* stats[0] units, [1] samples, [2] rice bits, [3] fixed units, [4] lpc units,
+ * [5..9] fixed order histogram, [10..42] lpc order histogram (index 10+order-1... 41),
+ * [48..63] partition order histogram, [64..79] status histogram, [80] residual checksum */
+int flacmi_stream_stats(flacmi_ctx* ctx, const flacmi_unit_meta* d_meta, int64_t n_units,
+                        int32_t block_len, int32_t tail_len, int64_t n_tail_units,
+                        int64_t* d_stats, void* stream);
+
+/* ---- synthetic PCM (BASELINE configs 2-5) --------------------------------- */
+/* Writes units [first_unit, first_unit + n_units) of the integer synthetic signal into
+ * dst[(u - first_unit) * unit_stride ...]: sum of 3 DDS sinusoids + splitmix64 noise,
+ * clipped to sample_bits; bit-identical to oracle/flac_oracle.c:oracle_synth_unit. */
+int flacmi_synth_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_t sample_bits,
+                        int64_t unit_stride, int64_t first_unit, int64_t n_units, int32_t len,
+                        uint64_t seed, void* stream);
+
+/* ---- device memory helpers (so hosts without a HIP binding can drive the device path) --- */
+void* flacmi_device_alloc(flacmi_ctx* ctx, size_t bytes);
+int flacmi_device_free(flacmi_ctx* ctx, void* ptr);
+int flacmi_memcpy_h2d(flacmi_ctx* ctx, void* dst, const void* src, size_t bytes);
+int flacmi_memcpy_d2h(flacmi_ctx* ctx, void* dst, const void* src, size_t bytes);
+int flacmi_synchronize(flacmi_ctx* ctx);
+
+/* ---- timing of the last flacmi_analyze_* call's kernels (HIP events on its stream) ---- */
+/* ms[0] acf+levinson kernels, ms[1] residual+rice kernels, ms[2] whole call; returns count */
+int flacmi_last_timing(flacmi_ctx* ctx, float* ms, int n);
+
+/* ---- host-side views of the device arithmetic (for CPU verification of the helpers) ---- */
+/* Python float `x ** 2` as CPython 3.10 + glibc 2.35 pow (FMA variant) computes it;
+ * *status receives FLACMI_STATUS_OVERFLOW where Python raises OverflowError. */
+double flacmi_host_pypow2(double x, int32_t* status);
+/* floor(math.log2(x)) for finite x > 0, via the threshold table the device uses
+ * (built once per process from libm log2). */
+int32_t flacmi_host_floor_log2(double x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLACMI_H */

@@ -1,0 +1,479 @@
+/*
+ * flac_oracle.c — CPU restatement of turlando/flac-py's encode-analysis hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see flac_oracle.h).  Written from the reference's
+ * behaviour, statement by statement, with the same IEEE operation sequence CPython 3.10
+ * executes: every float op is a separate double op (compiled with -ffp-contract=off),
+ * `sum()` over floats is a sequential left-to-right chain, and cos/log2/pow are the
+ * very libm functions CPython calls (reached through volatile pointers so GCC cannot
+ * fold pow(x, 2.0) into x*x).  Integer work uses int64/__int128 so nothing wraps.
+ * Python exceptions become (status, site) pairs, in the reference's evaluation order.
+ */
+#include "flac_oracle.h"
+
+#include <errno.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+static double (*volatile libm_cos)(double) = cos;
+static double (*volatile libm_log2)(double) = log2;
+static double (*volatile libm_pow)(double, double) = pow;
+static double (*volatile libm_sin)(double) = sin;
+
+/* math.pi */
+static const double PY_PI = 3.141592653589793;
+
+/* FIXED_PREDICTOR_COEFFICIENTS, flac/common.py:15-21 */
+static const int FIXED_COEFS[5][4] = {{0}, {1}, {2, -1}, {3, -3, 1}, {4, -6, 4, -1}};
+
+#define SET_ERR(st, si)          \
+    do {                         \
+        meta->status = (st);     \
+        meta->site = (si);       \
+        return (st);             \
+    } while (0)
+
+/* ------------------------------------------------------------------------------------
+ * Python float helpers
+ * ---------------------------------------------------------------------------------- */
+
+/* float.__pow__(x, 2) — CPython Objects/floatobject.c float_pow special cases, then libm
+ * pow(|x|, 2.0); ERANGE with an infinite result raises OverflowError. */
+double oracle_pypow2(double x, int32_t* status) {
+    *status = FLACMI_STATUS_OK;
+    if (isnan(x)) return x;
+    if (isinf(x)) return INFINITY;
+    if (x == 0.0) return 0.0;
+    double ax = fabs(x);
+    if (ax == 1.0) return 1.0;
+    errno = 0;
+    double r = libm_pow(ax, 2.0);
+    if (errno == 0 && isinf(r)) errno = ERANGE;
+    else if (errno == ERANGE && r == 0.0) errno = 0;
+    if (errno != 0) *status = FLACMI_STATUS_OVERFLOW;
+    return r;
+}
+
+/* math.floor(math.log2(x)) for a float x. */
+int32_t oracle_floor_log2(double x, int32_t* status) {
+    *status = FLACMI_STATUS_OK;
+    if (isnan(x)) { *status = FLACMI_STATUS_VALUE_ERROR; return 0; }
+    if (x <= 0.0) { *status = FLACMI_STATUS_VALUE_ERROR; return 0; } /* math domain error */
+    if (isinf(x)) { *status = FLACMI_STATUS_OVERFLOW; return 0; }   /* floor(inf) */
+    double l = libm_log2(x);
+    return (int32_t)floor(l);
+}
+
+/* ------------------------------------------------------------------------------------
+ * encoder.py:423-440 tukey(n, 0.5)
+ * ---------------------------------------------------------------------------------- */
+int oracle_tukey(int32_t n, double* w) {
+    int nr = (int)floor(0.25 * (double)n) - 1; /* floor(r / 2.0 * n) - 1, r = 0.5 */
+    for (int i = 0; i < n; i++) w[i] = 1.0;
+    for (int i = 0; i < nr + 1; i++) {
+        if (nr == 0) return FLACMI_SITE_TUKEY; /* pi * i / nr -> ZeroDivisionError */
+        w[i] = 0.5 - 0.5 * libm_cos(PY_PI * (double)i / (double)nr);
+        w[n - nr - 1 + i] = 0.5 - 0.5 * libm_cos(PY_PI * (double)(i + nr) / (double)nr);
+    }
+    return 0;
+}
+
+/* encoder.py:443-450: sum(samples[j] * samples[j+lag] for j in range(len - lag - 1)) */
+double oracle_autocorrelation(const double* x, int32_t n, int32_t lag) {
+    double s = 0.0;
+    for (int j = 0; j < n - lag - 1; j++) s += x[j] * x[j + lag];
+    return s;
+}
+
+/* encoder.py:453-479, called on r[0..order] (from scratch, as the reference does).
+ * coefs receives coefs[1:] (order values). */
+int oracle_levinson(const double* r, int32_t order, double* out, int32_t* site) {
+    double coefs[FLACMI_MAX_LPC_ORDER + 1];
+    *site = 0;
+    for (int i = 0; i <= order; i++) coefs[i] = 0.0;
+    coefs[0] = 1.0;
+    double error = r[0];
+    for (int k = 0; k < order; k++) {
+        double lambda = 0.0;
+        for (int j = 0; j < k + 1; j++) lambda -= coefs[j] * r[k + 1 - j];
+        if (error == 0.0) { *site = FLACMI_SITE_LEVINSON_DIV; return FLACMI_STATUS_ZERO_DIVISION; }
+        lambda /= error;
+        for (int nn = 0; nn < (k + 1) / 2 + 1; nn++) {
+            double temp = coefs[k + 1 - nn] + lambda * coefs[nn];
+            coefs[nn] = coefs[nn] + lambda * coefs[k + 1 - nn];
+            coefs[k + 1 - nn] = temp;
+        }
+        int32_t st;
+        double l2 = oracle_pypow2(lambda, &st);
+        if (st) { *site = FLACMI_SITE_LEVINSON_POW; return st; }
+        error *= 1.0 - l2;
+    }
+    for (int i = 0; i < order; i++) out[i] = coefs[i + 1];
+    return 0;
+}
+
+/* encoder.py:482-534 quantize_lpc_coefficients.  q receives the quantised list (nq values:
+ * n, or 0 in the negative-shift branch); *shift the returned shift. */
+int oracle_quantize(const double* c, int32_t n, int32_t precision, int32_t* q, int32_t* nq,
+                    int32_t* shift_out, int32_t* site) {
+    *site = 0;
+    *nq = 0;
+    /* coef_max = max([abs(x) for x in coefficients]) — builtin max keeps the first
+     * element unless a later one compares greater (NaN never does). */
+    double cmax = fabs(c[0]);
+    for (int i = 1; i < n; i++)
+        if (fabs(c[i]) > cmax) cmax = fabs(c[i]);
+    if (!(cmax > 0.0)) { *site = FLACMI_SITE_QUANT_CMAX; return FLACMI_STATUS_ASSERTION; }
+    int32_t st;
+    int32_t lg = oracle_floor_log2(cmax, &st);
+    if (st) { *site = FLACMI_SITE_QUANT_LOG2; return st; }
+    int shift_max = (1 << 4) - 1, shift_min = -(1 << 4);
+    int shift = precision - lg - 2;
+    if (shift > shift_max) shift = shift_max;
+    else if (shift < shift_min) { *site = FLACMI_SITE_QUANT_SHIFT; return FLACMI_STATUS_ASSERTION; }
+    double qmax = (double)((1LL << (precision - 1)) - 1);
+    double qmin = (double)(-(1LL << (precision - 1)));
+    double error = 0.0;
+    int neg = shift < 0;
+    double scale = ldexp(1.0, neg ? -shift : shift); /* 1 << shift, converted to float */
+    for (int i = 0; i < n; i++) {
+        error += c[i] * scale;
+        if (isinf(error)) { *site = FLACMI_SITE_QUANT_ROUND_INF; return FLACMI_STATUS_OVERFLOW; }
+        if (isnan(error)) { *site = FLACMI_SITE_QUANT_ROUND_NAN; return FLACMI_STATUS_VALUE_ERROR; }
+        double r = nearbyint(error); /* round() with no ndigits: half to even */
+        double qq = r < qmin ? qmin : (r > qmax ? qmax : r); /* clamp(round(e), min, max) */
+        error -= qq;
+        if (!neg) q[(*nq)++] = (int32_t)qq;
+    }
+    *shift_out = neg ? 0 : shift;
+    return 0;
+}
+
+/* encoder.py:537-548 prediction_residual: r[i] = x[i] - (sum(x[i-1-j]*c[j]) >> shift). */
+static void prediction_residual(const int64_t* x, int32_t n, const int32_t* c, int32_t nc,
+                                int32_t shift, int64_t* r) {
+    for (int i = nc; i < n; i++) {
+        __int128 s = 0;
+        for (int j = 0; j < nc; j++) s += (__int128)x[i - 1 - j] * c[j];
+        r[i - nc] = x[i] - (int64_t)(s >> shift);
+    }
+}
+
+static int64_t abs_sum(const int64_t* r, int32_t n) {
+    int64_t s = 0;
+    for (int i = 0; i < n; i++) s += r[i] < 0 ? -r[i] : r[i];
+    return s;
+}
+
+/* ------------------------------------------------------------------------------------
+ * encode_residual, encoder.py:632-760
+ * ---------------------------------------------------------------------------------- */
+static int encode_residual(const int64_t* res, int32_t res_len, int32_t block_size,
+                           int32_t predictor_order, const flacmi_params* p,
+                           flacmi_unit_meta* meta, int32_t* params_out, uint64_t* zz) {
+    for (int i = 0; i < res_len; i++) zz[i] = ((uint64_t)res[i] << 1) ^ (uint64_t)(res[i] >> 63);
+    int best_o = -1;
+    int64_t best_size = 0;
+    int32_t* cand_params = (int32_t*)malloc(sizeof(int32_t) * ((1 << FLACMI_MAX_RICE_ORDER) + 2));
+    int any = 0;
+    for (int o = p->rice_min; o <= p->rice_max; o++) {
+        if (!(block_size % (1 << o) == 0 && (block_size >> o) > predictor_order)) continue;
+        any = 1;
+        int32_t p0 = (block_size >> o) - predictor_order, ps = block_size >> o;
+        int64_t size = 0;
+        int np = 0;
+        int pos = 0;
+        while (pos < res_len) {
+            int len = np == 0 ? p0 : ps;
+            if (len > res_len - pos) len = res_len - pos;
+            uint64_t s = 0;
+            for (int i = 0; i < len; i++) s += zz[pos + i];
+            if (s == 0) { free(cand_params); SET_ERR(FLACMI_STATUS_VALUE_ERROR, FLACMI_SITE_RICE_LOG_DOMAIN); }
+            double mean = (double)s / (double)len; /* exact: s < 2^53 */
+            int32_t st;
+            int32_t param = oracle_floor_log2(mean, &st);
+            if (param < 0) { free(cand_params); SET_ERR(FLACMI_STATUS_VALUE_ERROR, FLACMI_SITE_RICE_NEG_SHIFT); }
+            int64_t bits = 0;
+            for (int i = 0; i < len; i++) bits += param >= 64 ? 0 : (int64_t)(zz[pos + i] >> param);
+            bits += (int64_t)len * (1 + param);
+            size += 4 + (param > 14 ? 5 : 4) + bits;
+            cand_params[np] = param;
+            np++;
+            pos += len;
+        }
+        if (best_o < 0 || size < best_size) {
+            best_o = o;
+            best_size = size;
+            memcpy(params_out, cand_params, sizeof(int32_t) * np);
+            meta->n_parts = np;
+        }
+    }
+    free(cand_params);
+    if (!any) SET_ERR(FLACMI_STATUS_ASSERTION, FLACMI_SITE_RICE_NO_ORDER);
+    meta->part_order = best_o;
+    meta->rice_bits = best_size;
+    int method = 4;
+    for (int i = 0; i < meta->n_parts; i++)
+        if (params_out[i] > 14) method = 5;
+    meta->coding_method = method;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------
+ * One unit: encode() lines 127-157 + writer's encode_residual call.
+ * ---------------------------------------------------------------------------------- */
+int oracle_analyze_unit(const int64_t* x, int32_t n, const flacmi_params* p,
+                        flacmi_unit_meta* meta, int32_t* rice_params, uint64_t* residual,
+                        double* acf, int64_t* fixed_sums, int64_t* lpc_sums, int32_t* lpc_record) {
+    memset(meta, 0, sizeof(*meta));
+    const int L = p->max_lpc_order;
+    int64_t* tmp = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 1) * 6);
+    int64_t* fres[5];
+    for (int k = 0; k < 5; k++) fres[k] = tmp + (size_t)k * (n + 1);
+    int64_t* lres = tmp + (size_t)5 * (n + 1);
+    int rc = 0;
+
+    /* ---- encode_subframe_fixed (encoder.py:331-359) ---- */
+    int64_t fsum[5] = {0, 0, 0, 0, 0};
+    int forder = 0;
+    if (n <= 4) {
+        for (int i = 0; i < n; i++) fres[0][i] = x[i];
+        fsum[0] = abs_sum(fres[0], n);
+    } else {
+        for (int k = 0; k < 5; k++) {
+            prediction_residual(x, n, FIXED_COEFS[k], k, 0, fres[k]);
+            fsum[k] = abs_sum(fres[k], n - k);
+        }
+        for (int k = 1; k < 5; k++)
+            if (fsum[k] < fsum[forder]) forder = k;
+    }
+    if (fixed_sums) memcpy(fixed_sums, fsum, sizeof(fsum));
+    meta->fixed_order = forder;
+    meta->fixed_sum = fsum[forder];
+
+    int kind = FLACMI_KIND_FIXED, order = forder, shift = 0, ncoefs = 0, res_offset = forder;
+    int32_t coefs[FLACMI_MAX_LPC_ORDER];
+    const int64_t* chosen = fres[forder];
+    int32_t chosen_len = n - (n <= 4 ? 0 : forder);
+    if (n <= 4) res_offset = 0;
+
+    if (p->mode == FLACMI_MODE_REFERENCE) {
+        /* ---- encode_subframe_lpc (encoder.py:362-420) ---- */
+        double* w = (double*)malloc(sizeof(double) * (size_t)n * 2);
+        double* win = w + n;
+        int tk = oracle_tukey(n, w);
+        if (tk) { free(w); meta->status = FLACMI_STATUS_ZERO_DIVISION; meta->site = tk; rc = meta->status; goto done; }
+        for (int i = 0; i < n; i++) win[i] = (double)x[i] * w[i];
+        double r[FLACMI_MAX_LPC_ORDER + 1];
+        for (int lag = 0; lag < L + 1; lag++) r[lag] = oracle_autocorrelation(win, n, lag);
+        free(w);
+        if (acf) {
+            for (int i = 0; i < 33; i++) acf[i] = 0.0;
+            for (int lag = 0; lag < L + 1; lag++) acf[lag] = r[lag];
+        }
+        /* 3. levinson_durbin(autocorrs[:i]) for i in 2..L+1 — all orders first */
+        double lc[FLACMI_MAX_LPC_ORDER][FLACMI_MAX_LPC_ORDER];
+        for (int ord = 1; ord <= L; ord++) {
+            int32_t site;
+            int st = oracle_levinson(r, ord, lc[ord - 1], &site);
+            if (st) { meta->status = st; meta->site = site; rc = st; goto done; }
+        }
+        /* 4. quantize every order */
+        int32_t qc[FLACMI_MAX_LPC_ORDER][FLACMI_MAX_LPC_ORDER], nq[FLACMI_MAX_LPC_ORDER],
+            qs[FLACMI_MAX_LPC_ORDER];
+        for (int ord = 1; ord <= L; ord++) {
+            int32_t site;
+            int st = oracle_quantize(lc[ord - 1], ord, p->qlp_precision, qc[ord - 1], &nq[ord - 1],
+                                     &qs[ord - 1], &site);
+            if (st) { meta->status = st; meta->site = site; rc = st; goto done; }
+        }
+        if (lpc_record) {
+            int words = FLACMI_LPC_REC_WORDS(32);
+            memset(lpc_record, 0, sizeof(int32_t) * words);
+            uint32_t negmask = 0;
+            for (int ord = 1; ord <= L; ord++) {
+                if (nq[ord - 1] == 0) negmask |= 1u << (ord - 1);
+                lpc_record[2 + ord - 1] = qs[ord - 1];
+                for (int j = 0; j < nq[ord - 1]; j++)
+                    lpc_record[2 + 32 + (ord * (ord - 1)) / 2 + j] = qc[ord - 1][j];
+            }
+            lpc_record[1] = (int32_t)negmask;
+        }
+        /* 5./6. residual and sum(|r|) per order; 7. first argmin */
+        if (L == 0) { meta->status = FLACMI_STATUS_VALUE_ERROR; meta->site = FLACMI_SITE_LPC_EMPTY; rc = meta->status; goto done; }
+        int best = -1;
+        int64_t best_sum = 0;
+        for (int ord = 1; ord <= L; ord++) {
+            int32_t len;
+            if (nq[ord - 1] == 0) { /* ([], 0): prediction_residual with no coefficients */
+                for (int i = 0; i < n; i++) lres[i] = x[i];
+                len = n;
+            } else {
+                prediction_residual(x, n, qc[ord - 1], nq[ord - 1], qs[ord - 1], lres);
+                len = n - nq[ord - 1];
+            }
+            int64_t s = abs_sum(lres, len > 0 ? len : 0);
+            if (lpc_sums) lpc_sums[ord - 1] = s;
+            if (best < 0 || s < best_sum) { best = ord; best_sum = s; }
+        }
+        meta->lpc_order = best;
+        meta->lpc_sum = best_sum;
+        /* ---- choice, encoder.py:135-157 ---- */
+        if (fsum[forder] < best_sum) {
+            /* fixed wins: already set */
+        } else if (best_sum < fsum[forder]) {
+            kind = FLACMI_KIND_LPC;
+            order = best;
+            shift = qs[best - 1];
+            ncoefs = nq[best - 1];
+            for (int j = 0; j < ncoefs; j++) coefs[j] = qc[best - 1][j];
+            if (ncoefs == 0) {
+                for (int i = 0; i < n; i++) lres[i] = x[i];
+                chosen_len = n;
+                res_offset = 0;
+            } else {
+                prediction_residual(x, n, coefs, ncoefs, shift, lres);
+                chosen_len = n - ncoefs;
+                res_offset = ncoefs;
+            }
+            chosen = lres;
+        } else {
+            meta->status = FLACMI_STATUS_ASSERTION;
+            meta->site = FLACMI_SITE_CHOICE_TIE;
+            rc = meta->status;
+            goto done;
+        }
+    }
+    meta->kind = kind;
+    meta->order = order;
+    meta->shift = shift;
+    meta->ncoefs = ncoefs;
+    for (int j = 0; j < ncoefs; j++) meta->coefs[j] = coefs[j];
+    meta->res_offset = res_offset;
+    meta->res_len = chosen_len;
+    {
+        uint64_t* zz = residual ? residual + res_offset : (uint64_t*)malloc(sizeof(uint64_t) * (size_t)n);
+        rc = encode_residual(chosen, chosen_len, n, order, p, meta, rice_params, zz);
+        if (!residual) free(zz);
+    }
+done:
+    free(tmp);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------------
+ * Batch driver (pthreads over units)
+ * ---------------------------------------------------------------------------------- */
+typedef struct {
+    const flacmi_batch* b;
+    const flacmi_params* p;
+    flacmi_unit_meta* meta;
+    int32_t* rice_params;
+    int64_t params_stride;
+    uint64_t* residual;
+    int64_t residual_stride;
+    double* acf;
+    int64_t* fixed_sums;
+    int64_t* lpc_sums;
+    int32_t* lpc_records;
+    int64_t begin, end;
+} job_t;
+
+static void* run_job(void* arg) {
+    job_t* j = (job_t*)arg;
+    const flacmi_batch* b = j->b;
+    int64_t* x = (int64_t*)malloc(sizeof(int64_t) * (size_t)(b->block_len > 0 ? b->block_len : 1));
+    for (int64_t u = j->begin; u < j->end; u++) {
+        int32_t n = (u >= b->n_units - b->n_tail_units) ? b->tail_len : b->block_len;
+        if (b->sample_bytes == 2) {
+            const int16_t* s = (const int16_t*)b->samples + u * b->unit_stride;
+            for (int i = 0; i < n; i++) x[i] = s[i];
+        } else {
+            const int32_t* s = (const int32_t*)b->samples + u * b->unit_stride;
+            for (int i = 0; i < n; i++) x[i] = s[i];
+        }
+        oracle_analyze_unit(x, n, j->p, &j->meta[u], j->rice_params + u * j->params_stride,
+                            j->residual ? j->residual + u * j->residual_stride : NULL,
+                            j->acf ? j->acf + u * 33 : NULL, j->fixed_sums ? j->fixed_sums + u * 5 : NULL,
+                            j->lpc_sums ? j->lpc_sums + u * 32 : NULL,
+                            j->lpc_records ? j->lpc_records + u * FLACMI_LPC_REC_WORDS(32) : NULL);
+    }
+    free(x);
+    return NULL;
+}
+
+int oracle_analyze_batch(const flacmi_batch* b, const flacmi_params* p, flacmi_unit_meta* meta,
+                         int32_t* rice_params, int64_t params_stride, uint64_t* residual,
+                         int64_t residual_stride, double* acf, int64_t* fixed_sums,
+                         int64_t* lpc_sums, int32_t* lpc_records, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    job_t jobs[256];
+    int64_t per = (b->n_units + threads - 1) / threads;
+    int started = 0;
+    for (int t = 0; t < threads; t++) {
+        job_t* j = &jobs[t];
+        j->b = b; j->p = p; j->meta = meta; j->rice_params = rice_params;
+        j->params_stride = params_stride; j->residual = residual; j->residual_stride = residual_stride;
+        j->acf = acf; j->fixed_sums = fixed_sums; j->lpc_sums = lpc_sums; j->lpc_records = lpc_records;
+        j->begin = t * per;
+        j->end = (t + 1) * per < b->n_units ? (t + 1) * per : b->n_units;
+        if (j->begin >= j->end) break;
+        if (threads == 1) { run_job(j); continue; }
+        pthread_create(&tid[t], NULL, run_job, j);
+        started++;
+    }
+    for (int t = 0; t < started; t++) pthread_join(tid[t], NULL);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------
+ * Synthetic signal, SURVEY §8d restated in integers (see flacmi_synth_device)
+ * ---------------------------------------------------------------------------------- */
+static uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+static int32_t sintab[4096];
+static pthread_once_t sintab_once = PTHREAD_ONCE_INIT;
+static void sintab_init(void) {
+    for (int k = 0; k < 4096; k++)
+        sintab[k] = (int32_t)nearbyint(32767.0 * libm_sin(6.283185307179586 * (double)k / 4096.0));
+}
+
+void oracle_synth_unit(int64_t unit, int32_t len, int32_t bits, uint64_t seed, int32_t* out) {
+    pthread_once(&sintab_once, sintab_init);
+    uint64_t h0 = splitmix64(seed ^ ((uint64_t)unit * 0xD1B54A32D192ED03ull));
+    int64_t amp[3];
+    uint32_t dphi[3], phi0[3];
+    for (int k = 0; k < 3; k++) {
+        uint64_t hk = splitmix64(h0 + (uint64_t)(k + 1));
+        amp[k] = 1638 + (int64_t)(hk % 8192);
+        uint64_t f = 20 + ((hk >> 16) % 7981);
+        dphi[k] = (uint32_t)((f << 32) / 44100);
+        phi0[k] = (uint32_t)(hk >> 32);
+    }
+    int64_t sigma = 66 + (int64_t)(splitmix64(h0 + 4) % 590);
+    int64_t lo = -(1LL << (bits - 1)), hi = (1LL << (bits - 1)) - 1;
+    for (int i = 0; i < len; i++) {
+        int64_t acc = 0;
+        for (int k = 0; k < 3; k++) acc += amp[k] * sintab[(uint32_t)(phi0[k] + (uint32_t)i * dphi[k]) >> 20];
+        int64_t s = acc >> 15;
+        uint64_t r = splitmix64(seed ^ ((uint64_t)unit << 32) ^ (uint64_t)i);
+        int64_t bsum = (int64_t)((r & 0xff) + ((r >> 8) & 0xff) + ((r >> 16) & 0xff) + ((r >> 24) & 0xff));
+        int64_t v = s + (((bsum - 510) * sigma) >> 7);
+        if (bits > 16) {
+            int e = bits - 16;
+            v = v * (1LL << e) + (int64_t)((r >> 32) & ((1ull << e) - 1)) - (1LL << (e - 1));
+        } else if (bits < 16) {
+            v >>= (16 - bits);
+        }
+        out[i] = (int32_t)(v < lo ? lo : (v > hi ? hi : v));
+    }
+}
