@@ -1,0 +1,45 @@
+"""Loader for libflacmi.so (the HIP kernels behind include/flacmi.h).
+
+There is no fallback: if the library is missing or no HIP device is present the
+calls fail loudly with FlacmiError.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+LIB_PATH = os.environ.get("FLACMI_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                     "libflacmi.so"))
+_lib = None
+
+
+class FlacmiError(RuntimeError):
+    """A libflacmi.so API call failed (argument, HIP runtime or unsupported shape)."""
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FlacmiError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; "
+                              f"g.build()'` (or make -C flac-py_amd/csrc)")
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in abi.SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.flacmi_abi_version()
+        if v != abi.ABI_VERSION:
+            raise FlacmiError(f"libflacmi ABI {v} != {abi.ABI_VERSION}")
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = "flacmi") -> None:
+    if rc != 0:
+        msg = load().flacmi_last_error().decode(errors="replace")
+        raise FlacmiError(f"{what} failed ({rc}): {msg}")
+
+
+def last_error() -> str:
+    return load().flacmi_last_error().decode(errors="replace")

@@ -1,0 +1,161 @@
+"""Batched encode-analysis on the GPU through libflacmi.so.
+
+`Analyzer` owns one flacmi context (one HIP device).  `analyze()` takes a 2-D array of
+planar units (one row per (block, channel)), runs fixed + LPC + choice + Rice search
+on the device and returns numpy views of the per-unit results (the fields of
+flac/common.py's SubframeHeader / SubframeFixed / SubframeLPC / Residual, see
+include/flacmi.h).  `analyze_device()` is the zero-copy form on device pointers used by
+bench.py.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from ._lib import FlacmiError, check, load
+
+
+def make_params(max_lpc_order: int, qlp_precision: int, rice_min: int, rice_max: int,
+                mode: int = abi.MODE_REFERENCE) -> abi.Params:
+    p = abi.Params()
+    p.max_lpc_order = max_lpc_order
+    p.qlp_precision = qlp_precision
+    p.rice_min = rice_min
+    p.rice_max = rice_max
+    p.mode = mode
+    return p
+
+
+def params_stride_for(rice_max: int) -> int:
+    return (1 << max(rice_max, 0)) + 1
+
+
+class Analyzer:
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.device = device
+        self.ctx = self.lib.flacmi_create(device)
+        if not self.ctx:
+            raise FlacmiError(f"flacmi_create({device}) failed: "
+                              f"{self.lib.flacmi_last_error().decode(errors='replace')}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.flacmi_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------------------
+    def analyze(self, samples: np.ndarray, params: abi.Params, block_len: int, tail_len: int = 0,
+                n_tail_units: int = 0, sample_bits: int = 16, residual_bytes: int = 4,
+                debug: bool = False) -> dict:
+        """Host arrays in, host arrays out (synchronous)."""
+        s = np.ascontiguousarray(samples)
+        if s.dtype not in (np.int16, np.int32) or s.ndim != 2:
+            raise ValueError("samples must be a 2-D int16 or int32 array")
+        n_units, stride = s.shape
+        b = abi.Batch()
+        b.samples = s.ctypes.data
+        b.sample_bytes = s.dtype.itemsize
+        b.sample_bits = sample_bits
+        b.unit_stride = stride
+        b.n_units = n_units
+        b.block_len = block_len
+        b.tail_len = tail_len
+        b.n_tail_units = n_tail_units
+        pstride = params_stride_for(params.rice_max)
+        rdt = np.uint32 if residual_bytes == 4 else np.uint64
+        rstride = ((block_len * residual_bytes + 15) // 16) * 16 // residual_bytes
+        out = {
+            "meta": np.zeros(n_units, dtype=abi.META_DTYPE),
+            "rice_params": np.zeros((n_units, pstride), dtype=np.int32),
+            "residual": np.zeros((n_units, rstride), dtype=rdt),
+        }
+        o = abi.Outputs()
+        o.meta = out["meta"].ctypes.data
+        o.rice_params = out["rice_params"].ctypes.data
+        o.params_stride = pstride
+        o.residual = out["residual"].ctypes.data
+        o.residual_bytes = residual_bytes
+        o.residual_stride = rstride
+        if debug:
+            out["acf"] = np.zeros((n_units, 33), dtype=np.float64)
+            out["fixed_sums"] = np.zeros((n_units, 5), dtype=np.int64)
+            out["lpc_sums"] = np.zeros((n_units, 32), dtype=np.int64)
+            out["lpc_records"] = np.zeros((n_units, abi.lpc_rec_words(32)), dtype=np.int32)
+            o.acf = out["acf"].ctypes.data
+            o.fixed_sums = out["fixed_sums"].ctypes.data
+            o.lpc_sums = out["lpc_sums"].ctypes.data
+            o.lpc_records = out["lpc_records"].ctypes.data
+        check(self.lib.flacmi_analyze_host(self.ctx, C.byref(b), C.byref(params), C.byref(o)),
+              "flacmi_analyze_host")
+        if residual_bytes == 4 and np.any(out["meta"]["status"] == abi.STATUS_RESIDUAL_WIDE):
+            # a chosen residual needs more than 32 bits: redo the batch with 64-bit rows
+            return self.analyze(samples, params, block_len, tail_len, n_tail_units, sample_bits, 8, debug)
+        return out
+
+    def analyze_device(self, samples_ptr: int, sample_bytes: int, sample_bits: int, unit_stride: int,
+                       n_units: int, block_len: int, params: abi.Params, meta_ptr: int,
+                       params_ptr: int, params_stride: int, residual_ptr: int, residual_stride: int,
+                       residual_bytes: int = 4, stream: int = 0, tail_len: int = 0,
+                       n_tail_units: int = 0) -> None:
+        """Device pointers in/out; enqueued on `stream`, returns without synchronising."""
+        b = abi.Batch()
+        b.samples = samples_ptr
+        b.sample_bytes = sample_bytes
+        b.sample_bits = sample_bits
+        b.unit_stride = unit_stride
+        b.n_units = n_units
+        b.block_len = block_len
+        b.tail_len = tail_len
+        b.n_tail_units = n_tail_units
+        o = abi.Outputs()
+        o.meta = meta_ptr
+        o.rice_params = params_ptr
+        o.params_stride = params_stride
+        o.residual = residual_ptr
+        o.residual_bytes = residual_bytes
+        o.residual_stride = residual_stride
+        check(self.lib.flacmi_analyze_device(self.ctx, C.byref(b), C.byref(params), C.byref(o), stream),
+              "flacmi_analyze_device")
+
+    def last_timing(self):
+        ms = (C.c_float * 3)()
+        k = self.lib.flacmi_last_timing(self.ctx, ms, 3)
+        if k < 0:
+            check(k, "flacmi_last_timing")
+        return list(ms)[:k]
+
+    def synth_device(self, dst_ptr: int, sample_bytes: int, sample_bits: int, unit_stride: int,
+                     first_unit: int, n_units: int, length: int, seed: int, stream: int = 0) -> None:
+        done = 0
+        while done < n_units:
+            k = min(65535, n_units - done)
+            check(self.lib.flacmi_synth_device(self.ctx, dst_ptr + done * unit_stride * sample_bytes,
+                                               sample_bytes, sample_bits, unit_stride, first_unit + done,
+                                               k, length, seed, stream), "flacmi_synth_device")
+            done += k
+
+    def stream_stats(self, meta_ptr: int, n_units: int, block_len: int, stats_ptr: int,
+                     stream: int = 0, tail_len: int = 0, n_tail_units: int = 0) -> None:
+        check(self.lib.flacmi_stream_stats(self.ctx, meta_ptr, n_units, block_len, tail_len,
+                                           n_tail_units, stats_ptr, stream), "flacmi_stream_stats")
+
+
+def unit_result(out: dict, i: int) -> dict:
+    """Per-unit dict view of analyze() results (the keys tests/golden_util.check reads)."""
+    m = out["meta"][i]
+    r = {name: int(m[name]) for name in abi.META_DTYPE.names if name != "coefs"}
+    r["coefs"] = [int(c) for c in m["coefs"][: int(m["ncoefs"])]]
+    r["rice_params"] = out["rice_params"][i][: int(m["n_parts"])]
+    off, ln = int(m["res_offset"]), int(m["res_len"])
+    r["residual"] = out["residual"][i][off: off + ln].astype(np.uint64)
+    for k in ("acf", "fixed_sums", "lpc_sums"):
+        r[k] = out[k][i] if k in out else None
+    r["lpc_record"] = out["lpc_records"][i] if "lpc_records" in out else None
+    return r

@@ -1,0 +1,546 @@
+/*
+ * flacmi_host.cpp — the C-ABI of libflacmi.so (include/flacmi.h): contexts, argument
+ * validation, per-length launch planning, tables computed from the host libm, and
+ * device-memory helpers.  All compute is in the HIP kernels (k_*.hip).
+ *
+ * Host-side tables (built with the same libm CPython uses, so the device sees exactly
+ * the values the reference computes):
+ *   - Tukey(0.5) window per block length (flac/encoder.py:423-440, libm cos);
+ *   - floor(log2(x)) thresholds per binary exponent (libm log2), for
+ *     quantize_lpc_coefficients (encoder.py:503) and find_rice_parameter (:753);
+ *   - the int16 sine table of the synthetic generator (libm sin).
+ * This file is compiled with -ffp-contract=off like the kernels.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/flacmi.h"
+#include "flacmi_kernels.h"
+#include "pymath.h"
+
+using namespace flacmi;
+
+static double (*volatile libm_cos)(double) = cos;
+static double (*volatile libm_log2)(double) = log2;
+static double (*volatile libm_sin)(double) = sin;
+
+/* ------------------------------------------------------------------------------------
+ * errors
+ * ---------------------------------------------------------------------------------- */
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(FLACMI_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                        __FILE__, __LINE__);                                            \
+    } while (0)
+
+/* ------------------------------------------------------------------------------------
+ * process-wide host tables
+ * ---------------------------------------------------------------------------------- */
+static std::once_flag g_tables_once;
+static std::vector<double> g_log2thr;   /* PYM_LOG2_THR_N */
+static std::vector<int32_t> g_sintab;   /* 4096 */
+static std::string g_tables_error;
+
+static void build_tables() {
+    g_log2thr.assign(PYM_LOG2_THR_N, 0.0);
+    for (int e = -1074; e <= 1023; ++e) {
+        const double hi = ldexp(1.0, e + 1); /* inf for e = 1023 */
+        double thr = hi;
+        {
+            double x = nextafter(hi, 0.0); /* DBL_MAX for e = 1023 */
+            while (x >= ldexp(1.0, e) && libm_log2(x) >= (double)(e + 1)) {
+                thr = x;
+                x = nextafter(x, 0.0);
+            }
+            /* monotonicity guard: nothing further below may reach e + 1 */
+            for (int k = 0; k < 64 && x >= ldexp(1.0, e); ++k, x = nextafter(x, 0.0))
+                if (libm_log2(x) >= (double)(e + 1)) g_tables_error = "libm log2 not monotonic near a power of two";
+        }
+        /* and nothing just above 2^e may fall below e */
+        double y = ldexp(1.0, e);
+        for (int k = 0; k < 64; ++k, y = nextafter(y, INFINITY))
+            if (libm_log2(y) < (double)e) g_tables_error = "libm log2 below the exponent just above 2^e";
+        g_log2thr[e + 1074] = thr;
+    }
+    g_sintab.resize(4096);
+    for (int k = 0; k < 4096; ++k)
+        g_sintab[k] = (int32_t)nearbyint(32767.0 * libm_sin(6.283185307179586 * (double)k / 4096.0));
+}
+
+static void ensure_tables() { std::call_once(g_tables_once, build_tables); }
+
+/* Tukey(0.5) window exactly as encoder.py:423-440 computes it; padded with zeros. */
+static std::vector<double> tukey_window(int n, int pad) {
+    std::vector<double> w((size_t)n + pad, 0.0);
+    for (int i = 0; i < n; ++i) w[i] = 1.0;
+    const int nr = (int)floor(0.25 * (double)n) - 1;
+    if (nr > 0) {
+        for (int i = 0; i < nr + 1; ++i) {
+            w[i] = 0.5 - 0.5 * libm_cos(3.141592653589793 * (double)i / (double)nr);
+            w[n - nr - 1 + i] = 0.5 - 0.5 * libm_cos(3.141592653589793 * (double)(i + nr) / (double)nr);
+        }
+    }
+    return w;
+}
+
+/* ------------------------------------------------------------------------------------
+ * context
+ * ---------------------------------------------------------------------------------- */
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct flacmi_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr; /* used by the host entry points */
+    double* d_log2thr = nullptr;
+    int32_t* d_sintab = nullptr;
+    std::map<int, double*> windows;
+    DevBuf rec, h_samples, h_meta, h_params, h_residual, h_acf, h_fs, h_ls, h_recs;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float last_ms[3] = {0, 0, 0};
+    bool timing_valid = false;
+};
+
+static int ensure_buf(DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return 0;
+    if (b.p) HIP_TRY(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t want = bytes + bytes / 8 + 4096;
+    HIP_TRY(hipMalloc(&b.p, want));
+    b.bytes = want;
+    return 0;
+}
+
+static int set_device(flacmi_ctx* ctx) {
+    HIP_TRY(hipSetDevice(ctx->device));
+    return 0;
+}
+
+extern "C" {
+
+int flacmi_abi_version(void) { return FLACMI_ABI_VERSION; }
+
+const char* flacmi_last_error(void) { return g_err.c_str(); }
+
+int flacmi_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+flacmi_ctx* flacmi_create(int device) {
+    ensure_tables();
+    if (!g_tables_error.empty()) {
+        fail(FLACMI_E_UNSUPPORTED, "%s", g_tables_error.c_str());
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        fail(FLACMI_E_HIP, "no HIP device available");
+        return nullptr;
+    }
+    if (device < 0 || device >= ndev) {
+        fail(FLACMI_E_INVALID, "device %d out of range (0..%d)", device, ndev - 1);
+        return nullptr;
+    }
+    flacmi_ctx* ctx = new flacmi_ctx();
+    ctx->device = device;
+    auto bad = [&](hipError_t e, const char* what) {
+        fail(FLACMI_E_HIP, "%s: %s", what, hipGetErrorString(e));
+        flacmi_destroy(ctx);
+        return (flacmi_ctx*)nullptr;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return bad(e, "hipSetDevice");
+    if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    for (auto& ev : ctx->ev)
+        if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipMalloc(&ctx->d_log2thr, sizeof(double) * PYM_LOG2_THR_N)) != hipSuccess) return bad(e, "hipMalloc");
+    if ((e = hipMemcpy(ctx->d_log2thr, g_log2thr.data(), sizeof(double) * PYM_LOG2_THR_N, hipMemcpyHostToDevice)) != hipSuccess)
+        return bad(e, "hipMemcpy");
+    if ((e = hipMalloc(&ctx->d_sintab, sizeof(int32_t) * 4096)) != hipSuccess) return bad(e, "hipMalloc");
+    if ((e = hipMemcpy(ctx->d_sintab, g_sintab.data(), sizeof(int32_t) * 4096, hipMemcpyHostToDevice)) != hipSuccess)
+        return bad(e, "hipMemcpy");
+    return ctx;
+}
+
+void flacmi_destroy(flacmi_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    for (auto& kv : ctx->windows) (void)hipFree(kv.second);
+    for (DevBuf* b : {&ctx->rec, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
+                      &ctx->h_fs, &ctx->h_ls, &ctx->h_recs})
+        if (b->p) (void)hipFree(b->p);
+    if (ctx->d_log2thr) (void)hipFree(ctx->d_log2thr);
+    if (ctx->d_sintab) (void)hipFree(ctx->d_sintab);
+    for (auto& ev : ctx->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+}  // extern "C"
+
+static int get_window(flacmi_ctx* ctx, int n, double** out) {
+    auto it = ctx->windows.find(n);
+    if (it != ctx->windows.end()) {
+        *out = it->second;
+        return 0;
+    }
+    std::vector<double> w = tukey_window(n, 64);
+    double* d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(double) * w.size()));
+    HIP_TRY(hipMemcpy(d, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice));
+    ctx->windows[n] = d;
+    *out = d;
+    return 0;
+}
+
+/* Largest candidate partition order for a block of n samples (predictor order 0). */
+static int rice_max_eff(int n, int rmin, int rmax) {
+    int r = -1;
+    for (int o = rmin; o <= rmax; ++o)
+        if (n % (1 << o) == 0) r = o;
+    return r;
+}
+
+static int validate(const flacmi_batch* b, const flacmi_params* p, const flacmi_outputs* o) {
+    if (!b || !p || !o) return fail(FLACMI_E_INVALID, "null argument");
+    if (b->sample_bytes != 2 && b->sample_bytes != 4) return fail(FLACMI_E_INVALID, "sample_bytes must be 2 or 4");
+    if (b->sample_bits < 2 || b->sample_bits > 8 * b->sample_bytes)
+        return fail(FLACMI_E_INVALID, "sample_bits %d invalid for %d-byte samples", b->sample_bits, b->sample_bytes);
+    if (b->n_units < 0 || b->n_tail_units < 0 || b->n_tail_units > b->n_units)
+        return fail(FLACMI_E_INVALID, "bad unit counts");
+    if (b->block_len < 1 || b->block_len > FLACMI_MAX_BLOCK) return fail(FLACMI_E_INVALID, "block_len out of range");
+    if (b->n_tail_units > 0 && (b->tail_len < 1 || b->tail_len > b->block_len))
+        return fail(FLACMI_E_INVALID, "tail_len out of range");
+    if (b->unit_stride < b->block_len) return fail(FLACMI_E_INVALID, "unit_stride < block_len");
+    if ((b->unit_stride * b->sample_bytes) % 16 != 0 || ((uintptr_t)b->samples % 16) != 0)
+        return fail(FLACMI_E_INVALID, "sample rows must be 16-byte aligned");
+    if (p->max_lpc_order < 0 || p->max_lpc_order > FLACMI_MAX_LPC_ORDER)
+        return fail(FLACMI_E_INVALID, "max_lpc_order must be 0..32");
+    if (p->qlp_precision < 5 || p->qlp_precision > 31) return fail(FLACMI_E_INVALID, "qlp_precision must be 5..31");
+    if (p->rice_min < 0 || p->rice_max > FLACMI_MAX_RICE_ORDER)
+        return fail(FLACMI_E_INVALID, "rice partition orders must be within 0..15");
+    if (p->mode != FLACMI_MODE_REFERENCE && p->mode != FLACMI_MODE_FIXED_ONLY) return fail(FLACMI_E_INVALID, "bad mode");
+    if (p->mode == FLACMI_MODE_REFERENCE && b->sample_bits + p->qlp_precision > 44)
+        return fail(FLACMI_E_UNSUPPORTED,
+                    "sample_bits + qlp_precision > 44: candidate residual sums may exceed int64 (see DESIGN.md)");
+    if (o->residual_bytes != 4 && o->residual_bytes != 8) return fail(FLACMI_E_INVALID, "residual_bytes must be 4 or 8");
+    if (o->residual_stride < b->block_len || (o->residual_stride * o->residual_bytes) % 16 != 0 ||
+        ((uintptr_t)o->residual % 16) != 0)
+        return fail(FLACMI_E_INVALID, "residual rows must hold block_len elements and be 16-byte aligned");
+    if (!o->meta || !o->rice_params || !o->residual) return fail(FLACMI_E_INVALID, "null output buffer");
+    const int lens[2] = {b->block_len, b->n_tail_units ? b->tail_len : b->block_len};
+    for (int n : lens) {
+        const int re = rice_max_eff(n, p->rice_min, p->rice_max);
+        if (re >= 0 && (1 << re) > kMaxFinestParts)
+            return fail(FLACMI_E_UNSUPPORTED, "2^%d Rice partitions exceed the %d this build stages in LDS", re,
+                        kMaxFinestParts);
+        if (re >= 0 && o->params_stride < (1 << re)) return fail(FLACMI_E_INVALID, "params_stride < 2^%d", re);
+        const ResidLaunch rl = resid_launch_config(n, re, o->residual_bytes);
+        if (rl.lds_bytes > 160 * 1024)
+            return fail(FLACMI_E_UNSUPPORTED, "block of %d samples needs %zu bytes of LDS", n, rl.lds_bytes);
+    }
+    return 0;
+}
+
+/* int32 arithmetic is exact when every |prediction| and |residual| < 2^29 (so an 8-sample
+ * partial sum of |r| also fits 32 bits); otherwise the kernels use int64. */
+static bool needs_wide(int bits, int L, int q, int mode) {
+    if (bits > 24 || q > 24) return true;
+    const double xmax = ldexp(1.0, bits - 1);
+    const double rmax = mode == FLACMI_MODE_FIXED_ONLY ? 16.0 * xmax : xmax * (1.0 + (double)L * ldexp(1.0, q - 1)) + 16.0 * xmax;
+    return rmax >= ldexp(1.0, 29);
+}
+
+static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi_params* p,
+                               const flacmi_outputs* o, hipStream_t s) {
+    if (int rc = set_device(ctx)) return rc;
+    const int L = p->mode == FLACMI_MODE_FIXED_ONLY ? 0 : p->max_lpc_order;
+    const int rec_words = FLACMI_LPC_REC_WORDS(L);
+    const bool wide = needs_wide(b->sample_bits, L, p->qlp_precision, p->mode);
+    if (p->mode == FLACMI_MODE_REFERENCE) {
+        if (int rc = ensure_buf(ctx->rec, sizeof(int32_t) * (size_t)rec_words * (size_t)(b->n_units > 0 ? b->n_units : 1)))
+            return rc;
+    }
+    struct Cls {
+        int64_t unit0, count;
+        int n;
+    } cls[2];
+    int ncls = 0;
+    const int64_t nfull = b->n_units - b->n_tail_units;
+    if (b->n_tail_units == 0 || b->tail_len == b->block_len) {
+        cls[ncls++] = {0, b->n_units, b->block_len};
+    } else {
+        if (nfull > 0) cls[ncls++] = {0, nfull, b->block_len};
+        cls[ncls++] = {nfull, b->n_tail_units, b->tail_len};
+    }
+    if (o->acf && p->mode != FLACMI_MODE_REFERENCE)
+        HIP_TRY(hipMemsetAsync(o->acf, 0, sizeof(double) * 33 * b->n_units, s));
+    HIP_TRY(hipEventRecord(ctx->ev[0], s));
+    /* LPC analysis for every class first, then the residual pass */
+    for (int c = 0; c < ncls && p->mode == FLACMI_MODE_REFERENCE; ++c) {
+        LpcArgs a{};
+        a.samples = b->samples;
+        a.stride = b->unit_stride;
+        a.unit0 = cls[c].unit0;
+        a.count = cls[c].count;
+        a.sample_bytes = b->sample_bytes;
+        a.n = cls[c].n;
+        a.L = L;
+        a.q = p->qlp_precision;
+        if (int rc = get_window(ctx, cls[c].n, (double**)&a.window)) return rc;
+        a.log2thr = ctx->d_log2thr;
+        a.rec = (int32_t*)ctx->rec.p + cls[c].unit0 * rec_words;
+        a.rec_words = rec_words;
+        a.acf = o->acf ? o->acf + cls[c].unit0 * 33 : nullptr;
+        HIP_TRY(launch_lpc(a, s));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    for (int c = 0; c < ncls; ++c) {
+        ResidArgs a{};
+        a.samples = b->samples;
+        a.stride = b->unit_stride;
+        a.unit0 = cls[c].unit0;
+        a.count = cls[c].count;
+        a.sample_bytes = b->sample_bytes;
+        a.n = cls[c].n;
+        a.L = L;
+        a.mode = p->mode;
+        a.rmin = p->rice_min;
+        a.rmax = p->rice_max;
+        a.rec = p->mode == FLACMI_MODE_REFERENCE ? (const int32_t*)ctx->rec.p + cls[c].unit0 * rec_words : nullptr;
+        a.rec_words = rec_words;
+        a.log2thr = ctx->d_log2thr;
+        a.meta = o->meta + cls[c].unit0;
+        a.rice_params = o->rice_params + cls[c].unit0 * o->params_stride;
+        a.params_stride = o->params_stride;
+        a.residual = (char*)o->residual + (size_t)cls[c].unit0 * o->residual_stride * o->residual_bytes;
+        a.residual_stride = o->residual_stride;
+        a.fixed_sums = o->fixed_sums ? o->fixed_sums + cls[c].unit0 * 5 : nullptr;
+        a.lpc_sums = o->lpc_sums ? o->lpc_sums + cls[c].unit0 * 32 : nullptr;
+        HIP_TRY(launch_resid(a, wide, o->residual_bytes, s));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    if (o->lpc_records) {
+        if (p->mode == FLACMI_MODE_REFERENCE) {
+            HIP_TRY(launch_expand_records((const int32_t*)ctx->rec.p, rec_words, L, b->n_units, o->lpc_records, s));
+        } else {
+            HIP_TRY(hipMemsetAsync(o->lpc_records, 0, sizeof(int32_t) * FLACMI_LPC_REC_WORDS(32) * b->n_units, s));
+        }
+    }
+    ctx->timing_valid = true;
+    return 0;
+}
+
+extern "C" {
+
+int flacmi_analyze_device(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_params* params,
+                          const flacmi_outputs* out, void* stream) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    if (int rc = validate(batch, params, out)) return rc;
+    if (batch->n_units == 0) return 0;
+    return analyze_device_impl(ctx, batch, params, out, (hipStream_t)stream);
+}
+
+int flacmi_analyze_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_params* params,
+                        const flacmi_outputs* out) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    if (!batch || !params || !out) return fail(FLACMI_E_INVALID, "null argument");
+    if (batch->n_units == 0) return 0;
+    if (int rc = set_device(ctx)) return rc;
+    const size_t nu = (size_t)batch->n_units;
+    /* device mirrors with 16-byte aligned rows */
+    const int64_t sstride = ((batch->block_len * batch->sample_bytes + 15) / 16) * 16 / batch->sample_bytes;
+    const int64_t rstride = ((batch->block_len * out->residual_bytes + 15) / 16) * 16 / out->residual_bytes;
+    if (int rc = ensure_buf(ctx->h_samples, nu * sstride * batch->sample_bytes)) return rc;
+    if (int rc = ensure_buf(ctx->h_meta, nu * sizeof(flacmi_unit_meta))) return rc;
+    if (int rc = ensure_buf(ctx->h_params, nu * out->params_stride * sizeof(int32_t))) return rc;
+    if (int rc = ensure_buf(ctx->h_residual, nu * rstride * out->residual_bytes)) return rc;
+    flacmi_batch db = *batch;
+    db.samples = ctx->h_samples.p;
+    db.unit_stride = sstride;
+    HIP_TRY(hipMemcpy2DAsync(ctx->h_samples.p, sstride * batch->sample_bytes, batch->samples,
+                             batch->unit_stride * batch->sample_bytes, batch->block_len * batch->sample_bytes, nu,
+                             hipMemcpyHostToDevice, ctx->stream));
+    flacmi_outputs dout = *out;
+    dout.meta = (flacmi_unit_meta*)ctx->h_meta.p;
+    dout.rice_params = (int32_t*)ctx->h_params.p;
+    dout.residual = ctx->h_residual.p;
+    dout.residual_stride = rstride;
+    if (out->acf) {
+        if (int rc = ensure_buf(ctx->h_acf, nu * 33 * sizeof(double))) return rc;
+        dout.acf = (double*)ctx->h_acf.p;
+    }
+    if (out->fixed_sums) {
+        if (int rc = ensure_buf(ctx->h_fs, nu * 5 * sizeof(int64_t))) return rc;
+        dout.fixed_sums = (int64_t*)ctx->h_fs.p;
+    }
+    if (out->lpc_sums) {
+        if (int rc = ensure_buf(ctx->h_ls, nu * 32 * sizeof(int64_t))) return rc;
+        dout.lpc_sums = (int64_t*)ctx->h_ls.p;
+    }
+    if (out->lpc_records) {
+        if (int rc = ensure_buf(ctx->h_recs, nu * FLACMI_LPC_REC_WORDS(32) * sizeof(int32_t))) return rc;
+        dout.lpc_records = (int32_t*)ctx->h_recs.p;
+    }
+    if (int rc = validate(&db, params, &dout)) return rc;
+    if (int rc = analyze_device_impl(ctx, &db, params, &dout, ctx->stream)) return rc;
+    HIP_TRY(hipMemcpyAsync(out->meta, dout.meta, nu * sizeof(flacmi_unit_meta), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(out->rice_params, dout.rice_params, nu * out->params_stride * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpy2DAsync(out->residual, out->residual_stride * out->residual_bytes, dout.residual,
+                             rstride * out->residual_bytes, batch->block_len * out->residual_bytes, nu,
+                             hipMemcpyDeviceToHost, ctx->stream));
+    if (out->acf)
+        HIP_TRY(hipMemcpyAsync(out->acf, dout.acf, nu * 33 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    if (out->fixed_sums)
+        HIP_TRY(hipMemcpyAsync(out->fixed_sums, dout.fixed_sums, nu * 5 * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    if (out->lpc_sums)
+        HIP_TRY(hipMemcpyAsync(out->lpc_sums, dout.lpc_sums, nu * 32 * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    if (out->lpc_records)
+        HIP_TRY(hipMemcpyAsync(out->lpc_records, dout.lpc_records, nu * FLACMI_LPC_REC_WORDS(32) * sizeof(int32_t),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int flacmi_stream_stats(flacmi_ctx* ctx, const flacmi_unit_meta* d_meta, int64_t n_units, int32_t block_len,
+                        int32_t tail_len, int64_t n_tail_units, int64_t* d_stats, void* stream) {
+    if (!ctx || !d_stats) return fail(FLACMI_E_INVALID, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(int64_t) * FLACMI_STATS_WORDS, (hipStream_t)stream));
+    HIP_TRY(launch_stats(d_meta, n_units, block_len, tail_len, n_tail_units, d_stats, (hipStream_t)stream));
+    return 0;
+}
+
+int flacmi_synth_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_t sample_bits, int64_t unit_stride,
+                        int64_t first_unit, int64_t n_units, int32_t len, uint64_t seed, void* stream) {
+    if (!ctx || !dst) return fail(FLACMI_E_INVALID, "null argument");
+    if (sample_bytes != 2 && sample_bytes != 4) return fail(FLACMI_E_INVALID, "sample_bytes must be 2 or 4");
+    if (sample_bits < 8 || sample_bits > 8 * sample_bytes || (sample_bits > 16 && sample_bits - 16 > 15))
+        return fail(FLACMI_E_INVALID, "sample_bits out of range");
+    if (len < 1 || unit_stride < len) return fail(FLACMI_E_INVALID, "bad length/stride");
+    if (n_units > 65535) return fail(FLACMI_E_INVALID, "at most 65535 units per synth call");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(launch_synth(dst, sample_bytes, sample_bits, unit_stride, first_unit, n_units, len, seed, ctx->d_sintab,
+                         (hipStream_t)stream));
+    return 0;
+}
+
+void* flacmi_device_alloc(flacmi_ctx* ctx, size_t bytes) {
+    if (!ctx) return nullptr;
+    if (set_device(ctx)) return nullptr;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+    if (e != hipSuccess) {
+        fail(FLACMI_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+int flacmi_device_free(flacmi_ctx* ctx, void* ptr) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipFree(ptr));
+    return 0;
+}
+
+int flacmi_memcpy_h2d(flacmi_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int flacmi_memcpy_d2h(flacmi_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int flacmi_synchronize(flacmi_ctx* ctx) {
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    return 0;
+}
+
+int flacmi_last_timing(flacmi_ctx* ctx, float* ms, int n) {
+    if (!ctx || !ctx->timing_valid) return fail(FLACMI_E_INVALID, "no timed call");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipEventSynchronize(ctx->ev[2]));
+    float t[3];
+    HIP_TRY(hipEventElapsedTime(&t[0], ctx->ev[0], ctx->ev[1]));
+    HIP_TRY(hipEventElapsedTime(&t[1], ctx->ev[1], ctx->ev[2]));
+    HIP_TRY(hipEventElapsedTime(&t[2], ctx->ev[0], ctx->ev[2]));
+    int k = n < 3 ? n : 3;
+    for (int i = 0; i < k; ++i) ms[i] = t[i];
+    return k;
+}
+
+double flacmi_host_pypow2(double x, int32_t* status) {
+    static const uint64_t lh[] = GLIBC_POW_LOG_HDR, lt[] = GLIBC_POW_LOG_TAB, eh[] = GLIBC_EXP_HDR,
+                          et[] = GLIBC_EXP_TAB;
+    const pym::PowTables T{lh, lt, eh, et};
+    int st = 0;
+    const double r = pym::py_pow2(x, T, &st);
+    if (status) *status = st;
+    return r;
+}
+
+int32_t flacmi_host_floor_log2(double x) {
+    ensure_tables();
+    return pym::py_floor_log2(x, g_log2thr.data());
+}
+
+int flacmi_device_selftest(flacmi_ctx* ctx, int32_t which, const double* x, double* out, int32_t* status,
+                           int64_t n) {
+    if (!ctx || !x || !out || !status) return fail(FLACMI_E_INVALID, "null argument");
+    if (which != 0 && which != 1) return fail(FLACMI_E_INVALID, "which must be 0 or 1");
+    if (n <= 0) return 0;
+    if (int rc = set_device(ctx)) return rc;
+    void* d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)n * (8 + 8 + 4)));
+    double* dx = (double*)d;
+    double* dout = dx + n;
+    int32_t* dst = (int32_t*)(dout + n);
+    int rc = 0;
+    hipError_t e = hipMemcpyAsync(dx, x, (size_t)n * 8, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = launch_selftest(which, dx, dout, dst, n, ctx->d_log2thr, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(status, dst, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) rc = fail(FLACMI_E_HIP, "selftest: %s", hipGetErrorString(e));
+    (void)hipFree(d);
+    return rc;
+}
+
+}  // extern "C"

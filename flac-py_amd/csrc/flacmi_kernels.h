@@ -1,0 +1,69 @@
+/*
+ * flacmi_kernels.h — internal interface between the host driver (flacmi_host.cpp) and
+ * the HIP kernels (flacmi_kernels.hip).  Not part of the public C-ABI.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/flacmi.h"
+
+namespace flacmi {
+
+/* One launch = one "length class": units [unit0, unit0 + count) that all have length n. */
+struct LpcArgs {
+    const void* samples;     /* batch base pointer */
+    int64_t stride;          /* elements between units */
+    int64_t unit0, count;
+    int32_t sample_bytes;
+    int32_t n, L, q;
+    const double* window;    /* [n] Tukey(0.5) window for this n (host libm cos) */
+    const double* log2thr;   /* [PYM_LOG2_THR_N] floor(log2) thresholds */
+    int32_t* rec;            /* [count][rec_words] LPC records (workspace) */
+    int32_t rec_words;
+    double* acf;             /* optional [count][33] */
+};
+
+struct ResidArgs {
+    const void* samples;
+    int64_t stride;
+    int64_t unit0, count;
+    int32_t sample_bytes;
+    int32_t n, L, mode;
+    int32_t rmin, rmax;      /* rice range; rmax < rmin => empty */
+    const int32_t* rec;      /* [count][rec_words] (NULL in fixed-only mode) */
+    int32_t rec_words;
+    const double* log2thr;
+    flacmi_unit_meta* meta;  /* [count] */
+    int32_t* rice_params;    /* [count][params_stride] */
+    int64_t params_stride;
+    void* residual;          /* [count][residual_stride] u32 or u64 */
+    int64_t residual_stride;
+    int64_t* fixed_sums;     /* optional [count][5] */
+    int64_t* lpc_sums;       /* optional [count][32] */
+};
+
+struct ResidLaunch {
+    int threads;             /* workgroup size (multiple of 64) */
+    size_t lds_bytes;        /* dynamic LDS */
+};
+
+/* Launch configuration the residual kernel needs for (n, L, rice range, residual width). */
+ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes);
+/* Largest partition order the LDS tables support. */
+constexpr int kMaxFinestParts = 4096;
+
+hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);
+hipError_t launch_resid(const ResidArgs& a, bool wide, int residual_bytes, hipStream_t s);
+hipError_t launch_expand_records(const int32_t* rec, int32_t rec_words, int32_t L, int64_t count,
+                                 int32_t* out, hipStream_t s);
+hipError_t launch_synth(void* dst, int32_t sample_bytes, int32_t bits, int64_t stride,
+                        int64_t first_unit, int64_t n_units, int32_t len, uint64_t seed,
+                        const int32_t* sintab, hipStream_t s);
+hipError_t launch_stats(const flacmi_unit_meta* meta, int64_t n_units, int32_t block_len,
+                        int32_t tail_len, int64_t n_tail_units, int64_t* stats, hipStream_t s);
+
+hipError_t launch_selftest(int32_t which, const double* x, double* out, int32_t* status, int64_t n,
+                           const double* log2thr, hipStream_t s);
+
+}  // namespace flacmi

@@ -1,0 +1,225 @@
+/* k_lpc.hip — autocorrelation + Levinson-Durbin + quantisation, one lane per unit
+ * (see device_common.h for the design notes). */
+#include "device_common.h"
+
+namespace flacmi {
+
+/* ====================================================================================
+ * k_lpc: autocorrelation + Levinson-Durbin + quantisation, one lane per unit
+ * ==================================================================================== */
+
+/* Load S consecutive samples starting at m0 (S multiple of 8, 16-byte aligned). */
+template <int S, typename SampleT>
+__device__ __forceinline__ void load_block(const SampleT* __restrict__ x, int m0, int M, bool full,
+                                           int32_t (&v)[S]) {
+    if (full) {
+        if constexpr (sizeof(SampleT) == 2) {
+#pragma unroll
+            for (int g = 0; g < S / 8; ++g) {
+                const short8 s = *reinterpret_cast<const short8*>(x + m0 + 8 * g);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[8 * g + k] = s[k];
+            }
+        } else {
+#pragma unroll
+            for (int g = 0; g < S / 4; ++g) {
+                const int4v s = *reinterpret_cast<const int4v*>(x + m0 + 4 * g);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[4 * g + k] = s[k];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < S; ++t) v[t] = (m0 + t < M) ? (int32_t)x[m0 + t] : 0;
+    }
+}
+
+template <int LMAX>
+__device__ __forceinline__ void write_quant(int32_t* rec, int L, int p, const int32_t* q, int nq,
+                                            int shift) {
+    rec[2 + p - 1] = shift;
+    int32_t* c = rec + 2 + L + (p * (p - 1)) / 2;
+#pragma unroll
+    for (int j = 0; j < LMAX; ++j)
+        if (j < p) c[j] = j < nq ? q[j] : 0;
+}
+
+template <int LMAX, typename SampleT>
+__global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= a.count) return;
+    const int64_t u = a.unit0 + gid;
+    const SampleT* __restrict__ x = (const SampleT*)a.samples + u * a.stride;
+    int32_t* __restrict__ rec = a.rec + gid * a.rec_words;
+    const int n = a.n, L = a.L, q = a.q;
+
+    if (n >= 4 && n <= 7) { /* tukey: nr == 0 -> pi * 0 / 0 (encoder.py:437) */
+        rec[0] = ST_ZERODIV | (FLACMI_SITE_TUKEY << 16);
+        rec[1] = 0;
+        if (a.acf)
+            for (int l = 0; l < 33; ++l) a.acf[gid * 33 + l] = 0.0;
+        return;
+    }
+
+    /* ---- autocorrelation: acc[l] = sum_{m} a[m-l] * a[m], m = 0 .. n-2 ---- */
+    constexpr int S = ((LMAX + 1 + 7) / 8) * 8;
+    double ring[S];
+    double acc[LMAX + 1];
+#pragma unroll
+    for (int t = 0; t < S; ++t) ring[t] = 0.0;
+#pragma unroll
+    for (int l = 0; l <= LMAX; ++l) acc[l] = 0.0;
+    const int M = n - 1; /* the last sample never enters a product (encoder.py:449) */
+    const int nblk = (M + S - 1) / S;
+    const double* __restrict__ win = a.window;
+    int32_t cur[S];
+    if (nblk > 0) load_block<S>(x, 0, M, S <= M, cur);
+    for (int b = 0; b < nblk; ++b) {
+        const int m0 = b * S;
+        int32_t nxt[S];
+        if (b + 1 < nblk) load_block<S>(x, m0 + S, M, m0 + 2 * S <= M, nxt);
+#pragma unroll
+        for (int t = 0; t < S; ++t) {
+            const double av = (double)cur[t] * win[m0 + t];
+            ring[t] = av;
+#pragma unroll
+            for (int l = 0; l <= LMAX; ++l) {
+                const double prev = ring[(t - l + S) % S];
+                acc[l] = acc[l] + prev * av;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < S; ++t) cur[t] = nxt[t];
+    }
+    if (a.acf) {
+        double* o = a.acf + gid * 33;
+#pragma unroll
+        for (int l = 0; l < 33; ++l) o[l] = (l <= LMAX && l <= L) ? acc[l < LMAX ? l : LMAX] : 0.0;
+    }
+
+    /* ---- Levinson-Durbin at max order with a snapshot per order (encoder.py:453-479) ---- */
+    const pym::PowTables PT{c_log_hdr, c_log_tab, c_exp_hdr, c_exp_tab};
+    double c[LMAX + 1];
+    c[0] = 1.0;
+#pragma unroll
+    for (int j = 1; j <= LMAX; ++j) c[j] = 0.0;
+    double err = acc[0];
+    int lst = ST_OK, lsite = 0, qst = ST_OK, qsite = 0;
+    uint32_t negmask = 0;
+    const double qmax = (double)((1LL << (q - 1)) - 1);
+    const double qmin = -(double)(1LL << (q - 1));
+    static_for<LMAX>([&](auto K_) {
+        constexpr int k = K_;
+        if (k < L && lst == ST_OK) {
+            double lam = 0.0;
+#pragma unroll
+            for (int j = 0; j <= k; ++j) lam = lam - c[j] * acc[k + 1 - j];
+            if (err == 0.0) {
+                lst = ST_ZERODIV;
+                lsite = FLACMI_SITE_LEVINSON_DIV;
+            } else {
+                lam = lam / err;
+#pragma unroll
+                for (int nn = 0; nn <= (k + 1) / 2; ++nn) {
+                    const double tmp = c[k + 1 - nn] + lam * c[nn];
+                    c[nn] = c[nn] + lam * c[k + 1 - nn];
+                    c[k + 1 - nn] = tmp;
+                }
+                int pst;
+                const double l2 = pym::py_pow2(lam, PT, &pst);
+                if (pst) {
+                    lst = ST_OVERFLOW;
+                    lsite = FLACMI_SITE_LEVINSON_POW;
+                } else {
+                    err = err * (1.0 - l2);
+                }
+            }
+            /* quantise order p = k + 1 (encoder.py:482-534) unless an earlier order failed */
+            if (lst == ST_OK && qst == ST_OK) {
+                const int p = k + 1;
+                double cm = __builtin_fabs(c[1]);
+#pragma unroll
+                for (int j = 2; j <= LMAX; ++j)
+                    if (j <= p && __builtin_fabs(c[j]) > cm) cm = __builtin_fabs(c[j]);
+                int32_t qv[LMAX];
+                int nq = 0, shift = 0;
+                if (!(cm > 0.0)) {
+                    qst = ST_ASSERT;
+                    qsite = FLACMI_SITE_QUANT_CMAX;
+                } else if (__builtin_isinf(cm)) {
+                    qst = ST_OVERFLOW;
+                    qsite = FLACMI_SITE_QUANT_LOG2;
+                } else {
+                    shift = q - pym::py_floor_log2(cm, a.log2thr) - 2;
+                    if (shift > 15) shift = 15;
+                    if (shift < -16) {
+                        qst = ST_ASSERT;
+                        qsite = FLACMI_SITE_QUANT_SHIFT;
+                    } else {
+                        const bool neg = shift < 0;
+                        const double scale = pow2_exact(neg ? -shift : shift);
+                        double e = 0.0;
+#pragma unroll
+                        for (int j = 1; j <= LMAX; ++j) {
+                            if (j <= p && qst == ST_OK) {
+                                e = e + c[j] * scale;
+                                if (__builtin_isinf(e)) {
+                                    qst = ST_OVERFLOW;
+                                    qsite = FLACMI_SITE_QUANT_ROUND_INF;
+                                } else if (__builtin_isnan(e)) {
+                                    qst = ST_VALUE;
+                                    qsite = FLACMI_SITE_QUANT_ROUND_NAN;
+                                } else {
+                                    const double r = __builtin_rint(e);
+                                    const double qq = r < qmin ? qmin : (r > qmax ? qmax : r);
+                                    e = e - qq;
+                                    qv[j - 1] = (int32_t)qq;
+                                }
+                            }
+                        }
+                        if (qst == ST_OK) {
+                            if (neg) {
+                                negmask |= 1u << k;
+                                shift = 0;
+                                nq = 0;
+                            } else {
+                                nq = p;
+                            }
+                            write_quant<LMAX>(rec, L, p, qv, nq, shift);
+                        }
+                    }
+                }
+            }
+        }
+    });
+    int st = lst != ST_OK ? lst : qst;
+    int site = lst != ST_OK ? lsite : qsite;
+    if (st == ST_OK && L == 0) { /* min() over no candidates (encoder.py:404) */
+        st = ST_VALUE;
+        site = FLACMI_SITE_LPC_EMPTY;
+    }
+    rec[0] = st | (site << 16);
+    rec[1] = (int32_t)negmask;
+}
+
+template <int LMAX>
+static hipError_t launch_lpc_T(const LpcArgs& a, hipStream_t s) {
+    const dim3 grid((unsigned)((a.count + 255) / 256));
+    if (a.sample_bytes == 2)
+        hipLaunchKernelGGL((k_lpc<LMAX, int16_t>), grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_lpc<LMAX, int32_t>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_lpc(const LpcArgs& a, hipStream_t s) {
+    if (a.count <= 0) return hipSuccess;
+    if (a.L <= 4) return launch_lpc_T<4>(a, s);
+    if (a.L <= 8) return launch_lpc_T<8>(a, s);
+    if (a.L <= 12) return launch_lpc_T<12>(a, s);
+    if (a.L <= 16) return launch_lpc_T<16>(a, s);
+    return launch_lpc_T<32>(a, s);
+}
+
+
+}  // namespace flacmi

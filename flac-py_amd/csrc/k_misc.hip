@@ -1,0 +1,184 @@
+/* k_misc.hip — small kernels (record expansion, synthetic PCM, stream statistics) and
+ * the residual-kernel dispatch. */
+#include "device_common.h"
+
+namespace flacmi {
+
+hipError_t launch_resid_l0(const ResidArgs&, bool, int, hipStream_t);
+hipError_t launch_resid_l8(const ResidArgs&, bool, int, hipStream_t);
+hipError_t launch_resid_l12(const ResidArgs&, bool, int, hipStream_t);
+hipError_t launch_resid_l16(const ResidArgs&, bool, int, hipStream_t);
+hipError_t launch_resid_l32(const ResidArgs&, bool, int, hipStream_t);
+
+/* ====================================================================================
+ * small kernels: record expansion (debug), synthetic PCM, stream statistics
+ * ==================================================================================== */
+__global__ void k_expand_records(const int32_t* rec, int32_t rec_words, int32_t L, int64_t count,
+                                 int32_t* out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= count) return;
+    const int32_t* r = rec + gid * rec_words;
+    int32_t* o = out + gid * FLACMI_LPC_REC_WORDS(32);
+    for (int i = 0; i < FLACMI_LPC_REC_WORDS(32); ++i) o[i] = 0;
+    o[0] = r[0];
+    o[1] = r[1];
+    if ((r[0] & 0xffff) != 0) return;
+    for (int pp = 1; pp <= L; ++pp) {
+        o[2 + pp - 1] = r[2 + pp - 1];
+        for (int j = 0; j < pp; ++j) o[2 + 32 + (pp * (pp - 1)) / 2 + j] = r[2 + L + (pp * (pp - 1)) / 2 + j];
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+/* SURVEY §8d synthetic signal; identical integer recipe to oracle_synth_unit. */
+template <typename T>
+__global__ __launch_bounds__(256) void k_synth(T* dst, int32_t bits, int64_t stride, int64_t first_unit,
+                                               int32_t len, uint64_t seed, const int32_t* __restrict__ sintab) {
+    const int64_t uu = blockIdx.y;
+    const int64_t unit = first_unit + uu;
+    const uint64_t h0 = splitmix64(seed ^ ((uint64_t)unit * 0xD1B54A32D192ED03ull));
+    int64_t amp[3];
+    uint32_t dphi[3], phi0[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint64_t hk = splitmix64(h0 + (uint64_t)(k + 1));
+        amp[k] = 1638 + (int64_t)(hk % 8192);
+        const uint64_t f = 20 + ((hk >> 16) % 7981);
+        dphi[k] = (uint32_t)((f << 32) / 44100);
+        phi0[k] = (uint32_t)(hk >> 32);
+    }
+    const int64_t sigma = 66 + (int64_t)(splitmix64(h0 + 4) % 590);
+    const int64_t lo = -(1LL << (bits - 1)), hi = (1LL << (bits - 1)) - 1;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < len; i += gridDim.x * 256) {
+        int64_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc += amp[k] * sintab[(uint32_t)(phi0[k] + (uint32_t)i * dphi[k]) >> 20];
+        const int64_t s = acc >> 15;
+        const uint64_t r = splitmix64(seed ^ ((uint64_t)unit << 32) ^ (uint64_t)i);
+        const int64_t bsum = (int64_t)((r & 0xff) + ((r >> 8) & 0xff) + ((r >> 16) & 0xff) + ((r >> 24) & 0xff));
+        int64_t v = s + (((bsum - 510) * sigma) >> 7);
+        if (bits > 16) {
+            const int e = bits - 16;
+            v = v * (1LL << e) + (int64_t)((r >> 32) & ((1ull << e) - 1)) - (1LL << (e - 1));
+        } else if (bits < 16) {
+            v >>= (16 - bits);
+        }
+        dst[uu * stride + i] = (T)(v < lo ? lo : (v > hi ? hi : v));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_stats(const flacmi_unit_meta* __restrict__ meta, int64_t n_units,
+                                               int32_t block_len, int32_t tail_len, int64_t n_tail_units,
+                                               unsigned long long* stats) {
+    __shared__ unsigned long long h[FLACMI_STATS_WORDS];
+    for (int i = threadIdx.x; i < FLACMI_STATS_WORDS; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += (int64_t)gridDim.x * blockDim.x) {
+        const flacmi_unit_meta& m = meta[u];
+        const int n = u >= n_units - n_tail_units ? tail_len : block_len;
+        atomicAdd(&h[0], 1ull);
+        atomicAdd(&h[1], (unsigned long long)n);
+        const int st = m.status & 15;
+        atomicAdd(&h[64 + (m.status >= 16 ? 15 : st)], 1ull);
+        if (m.status != 0) continue;
+        atomicAdd(&h[2], (unsigned long long)m.rice_bits);
+        if (m.kind == FLACMI_KIND_FIXED) {
+            atomicAdd(&h[3], 1ull);
+            atomicAdd(&h[5 + (m.order & 7) % 5], 1ull);
+        } else {
+            atomicAdd(&h[4], 1ull);
+            atomicAdd(&h[9 + (m.order >= 1 && m.order <= 32 ? m.order : 32)], 1ull);
+        }
+        atomicAdd(&h[48 + (m.part_order & 15)], 1ull);
+        unsigned long long hsh = (unsigned long long)m.rice_bits * 0x9E3779B97F4A7C15ull ^
+                                 ((unsigned long long)m.fixed_sum << 1) ^ (unsigned long long)m.lpc_sum;
+        atomicAdd(&h[80], hsh);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < FLACMI_STATS_WORDS; i += blockDim.x)
+        if (h[i]) atomicAdd(&stats[i], h[i]);
+}
+
+static int lmax_bucket(int L) { return L <= 0 ? 0 : L <= 8 ? 8 : L <= 12 ? 12 : L <= 16 ? 16 : 32; }
+
+ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes) {
+    const int nch = (n + 7) / 8;
+    int nt = 64 * ((nch + 64 * kCPT - 1) / (64 * kCPT));
+    if (nt < 64) nt = 64;
+    ResidLaunch r;
+    r.threads = nt;
+    r.lds_bytes = resid_lds_bytes(32, n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff), residual_bytes == 8 ? 8 : 4);
+    return r;
+}
+
+hipError_t launch_resid(const ResidArgs& a, bool wide, int residual_bytes, hipStream_t s) {
+    if (a.count <= 0) return hipSuccess;
+    const int lb = a.mode == FLACMI_MODE_FIXED_ONLY ? 0 : lmax_bucket(a.L);
+    switch (lb) {
+        case 0: return launch_resid_l0(a, wide, residual_bytes, s);
+        case 8: return launch_resid_l8(a, wide, residual_bytes, s);
+        case 12: return launch_resid_l12(a, wide, residual_bytes, s);
+        case 16: return launch_resid_l16(a, wide, residual_bytes, s);
+        default: return launch_resid_l32(a, wide, residual_bytes, s);
+    }
+}
+
+hipError_t launch_expand_records(const int32_t* rec, int32_t rec_words, int32_t L, int64_t count,
+                                 int32_t* out, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_expand_records, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, rec,
+                       rec_words, L, count, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth(void* dst, int32_t sample_bytes, int32_t bits, int64_t stride, int64_t first_unit,
+                        int64_t n_units, int32_t len, uint64_t seed, const int32_t* sintab, hipStream_t s) {
+    if (n_units <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((len + 255) / 256), (unsigned)n_units);
+    if (sample_bytes == 2)
+        hipLaunchKernelGGL(k_synth<int16_t>, grid, dim3(256), 0, s, (int16_t*)dst, bits, stride, first_unit, len, seed, sintab);
+    else
+        hipLaunchKernelGGL(k_synth<int32_t>, grid, dim3(256), 0, s, (int32_t*)dst, bits, stride, first_unit, len, seed, sintab);
+    return hipGetLastError();
+}
+
+hipError_t launch_stats(const flacmi_unit_meta* meta, int64_t n_units, int32_t block_len, int32_t tail_len,
+                        int64_t n_tail_units, int64_t* stats, hipStream_t s) {
+    if (n_units <= 0) return hipSuccess;
+    int64_t blocks = (n_units + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(k_stats, dim3((unsigned)blocks), dim3(256), 0, s, meta, n_units, block_len, tail_len,
+                       n_tail_units, (unsigned long long*)stats);
+    return hipGetLastError();
+}
+
+__global__ void k_selftest(int32_t which, const double* __restrict__ x, double* __restrict__ out,
+                           int32_t* __restrict__ status, int64_t n, const double* __restrict__ log2thr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (which == 0) {
+        const pym::PowTables PT{c_log_hdr, c_log_tab, c_exp_hdr, c_exp_tab};
+        int st = 0;
+        out[i] = pym::py_pow2(x[i], PT, &st);
+        status[i] = st;
+    } else {
+        out[i] = (double)pym::py_floor_log2(x[i], log2thr);
+        status[i] = 0;
+    }
+}
+
+hipError_t launch_selftest(int32_t which, const double* x, double* out, int32_t* status, int64_t n,
+                           const double* log2thr, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, which, x, out, status, n,
+                       log2thr);
+    return hipGetLastError();
+}
+
+}  // namespace flacmi

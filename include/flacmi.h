@@ -213,6 +213,12 @@ double flacmi_host_pypow2(double x, int32_t* status);
  * (built once per process from libm log2). */
 int32_t flacmi_host_floor_log2(double x);
 
+/* The same helpers executed by the device kernels, over n host inputs (synchronous):
+ * which = 0: out[i] = x[i] ** 2 (status[i] as flacmi_host_pypow2);
+ * which = 1: out[i] = floor(log2(x[i])) for finite x[i] > 0. */
+int flacmi_device_selftest(flacmi_ctx* ctx, int32_t which, const double* x, double* out,
+                           int32_t* status, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

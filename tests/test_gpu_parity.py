@@ -1,0 +1,194 @@
+"""Device (libflacmi.so HIP kernels) vs the reference's golden vectors and vs the CPU
+oracle, bit-exact: autocorrelation (float.hex), every LPC candidate, sums, choice,
+residuals, Rice parameters — and the same Python exceptions."""
+import math
+import random
+
+import numpy as np
+import pytest
+
+import golden_util as G
+import oracle
+from flac_amd import abi
+from flac_amd.analysis import Analyzer, make_params, unit_result
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def az():
+    a = Analyzer(0)
+    yield a
+    a.close()
+
+
+def run_units(az, units, n, params, bits=16, tail=None, debug=True, residual_bytes=4):
+    """units: list of int lists, all of length n except the optional trailing `tail` ones."""
+    dt = np.int16 if bits <= 16 else np.int32
+    stride = ((n * np.dtype(dt).itemsize + 15) // 16) * 16 // np.dtype(dt).itemsize
+    a = np.zeros((len(units), stride), dtype=dt)
+    for i, u in enumerate(units):
+        a[i, :len(u)] = u
+    ntail = 0 if tail is None else tail[1]
+    tlen = 0 if tail is None else tail[0]
+    return az.analyze(a, params, n, tlen, ntail, sample_bits=bits, residual_bytes=residual_bytes, debug=debug)
+
+
+# ---------------------------------------------------------------------------------------
+# golden fixtures (produced by the reference itself)
+# ---------------------------------------------------------------------------------------
+def _golden_cases():
+    for s in ["c1.json", "c2.json", "c3.json", "c5.json", "edge.json"]:
+        d = G.load(s)
+        for i, e in enumerate(d["units"]):
+            tag = e["source"].get("tag") or f"u{e['source'].get('unit', i)}"
+            yield pytest.param(e, id=f"{s[:-5]}-{i}-{tag}"[:60])
+
+
+@pytest.mark.parametrize("entry", list(_golden_cases()))
+def test_device_matches_reference_golden(az, entry):
+    xs = G.samples_for(entry, oracle.synth_unit)
+    bits = entry["params"]["sample_size"] if entry["source"]["kind"] == "synth" else 16
+    bits = max(bits, max((abs(v) for v in xs), default=0).bit_length() + 1)
+    out = run_units(az, [xs], len(xs), make_params(**G.params_of(entry)), bits=bits)
+    res = unit_result(out, 0)
+    bad = G.check(res, entry)
+    assert not bad, "\n".join(bad)
+
+
+# ---------------------------------------------------------------------------------------
+# batches vs the oracle
+# ---------------------------------------------------------------------------------------
+def compare_with_oracle(out, ora, lens):
+    gm, om = out["meta"], ora["meta"]
+    fields = [f for f in abi.META_DTYPE.names if f not in ("coefs", "reserved0")]
+    for u, n in enumerate(lens):
+        st = int(om["status"][u])
+        assert int(gm["status"][u]) == st, (u, "status", int(gm["status"][u]), st)
+        assert int(gm["site"][u]) == int(om["site"][u]), (u, "site")
+        if st != 0:
+            continue
+        for f in fields:
+            assert gm[f][u] == om[f][u], (u, f, gm[f][u], om[f][u])
+        k = int(om["ncoefs"][u])
+        assert list(gm["coefs"][u][:k]) == list(om["coefs"][u][:k]), (u, "coefs")
+        npart = int(om["n_parts"][u])
+        assert np.array_equal(out["rice_params"][u][:npart], ora["rice_params"][u][:npart]), (u, "params")
+        off, ln = int(om["res_offset"][u]), int(om["res_len"][u])
+        assert np.array_equal(out["residual"][u][off:off + ln].astype(np.uint64),
+                              ora["residual"][u][off:off + ln]), (u, "residual")
+        if "acf" in out:
+            assert np.array_equal(out["acf"][u].view(np.uint64), ora["acf"][u].view(np.uint64)), (u, "acf")
+            assert np.array_equal(out["fixed_sums"][u], ora["fixed_sums"][u]), (u, "fixed_sums")
+            assert np.array_equal(out["lpc_sums"][u], ora["lpc_sums"][u]), (u, "lpc_sums")
+            assert np.array_equal(out["lpc_records"][u], ora["lpc_records"][u]), (u, "lpc_records")
+
+
+def batch_case(az, n_units, n, bits, seed, L, q, rmin, rmax, mode=abi.MODE_REFERENCE, tail=None, threads=16):
+    dt = np.int16 if bits <= 16 else np.int32
+    a = oracle.synth_batch(0, n_units, n, bits, seed, dtype=dt)
+    if tail:
+        tl, tn = tail
+        a[n_units - tn:, tl:] = 0
+    p = make_params(L, q, rmin, rmax, mode)
+    out = az.analyze(a, p, n, tail[0] if tail else 0, tail[1] if tail else 0, sample_bits=bits, debug=True)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, q, rmin, rmax, mode), n, tail[0] if tail else 0,
+                               tail[1] if tail else 0, sample_bits=bits, threads=threads)
+    lens = [n] * n_units
+    if tail:
+        for i in range(n_units - tail[1], n_units):
+            lens[i] = tail[0]
+    compare_with_oracle(out, ora, lens)
+    return out
+
+
+def test_c2_shape_batch(az):
+    """BASELINE config 2 shape: 4608 x int16, -l 12 -q 5 -r 0,5."""
+    batch_case(az, 192, 4608, 16, 2024, 12, 5, 0, 5)
+
+
+def test_c1_params_with_short_tail(az):
+    """config 1 parameters with a stream's short last block (3240 samples)."""
+    batch_case(az, 40, 4608, 16, 7, 8, 5, 0, 5, tail=(3240, 1))
+
+
+def test_c3_shape_batch(az):
+    """BASELINE config 3 shape: 16384 x 24-bit, -l 32 -q 15 -r 0,8."""
+    batch_case(az, 12, 16384, 24, 96, 32, 15, 0, 8)
+
+
+def test_c5_fixed_only_batch(az):
+    batch_case(az, 256, 4608, 16, 55, 0, 5, 0, 5, mode=abi.MODE_FIXED_ONLY)
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 5, 8, 11, 13, 16, 20, 24, 31, 32])
+def test_every_order_bucket(az, L):
+    batch_case(az, 24, 1152, 16, 100 + L, L, 5 + (L % 9), 0, 6)
+
+
+def test_random_edge_units(az):
+    """Small random blocks of every length 1..64 and odd params: statuses, sites and
+    results all equal the oracle's (which the golden tests pin to the reference)."""
+    rnd = random.Random(7)
+    for trial in range(40):
+        n = rnd.randint(1, 64)
+        L = rnd.choice([0, 1, 2, 4, 8, 12])
+        q = rnd.choice([5, 6, 9, 15])
+        rmin = rnd.choice([0, 0, 1, 2])
+        rmax = rnd.choice([rmin - 1, rmin, rmin + 2, 6])
+        mode = rnd.choice([abi.MODE_REFERENCE, abi.MODE_REFERENCE, abi.MODE_FIXED_ONLY])
+        amp = rnd.choice([0, 1, 3, 100, 30000])
+        units = [[rnd.randint(-amp, amp) for _ in range(n)] for _ in range(8)]
+        a = np.zeros((8, ((n + 7) // 8) * 8), dtype=np.int16)
+        for i, u in enumerate(units):
+            a[i, :n] = u
+        if rmax < rmin:
+            rmax_c = rmin - 1
+        else:
+            rmax_c = rmax
+        p = make_params(L, q, rmin, rmax_c, mode)
+        out = az.analyze(a, p, n, sample_bits=16, debug=True)
+        ora = oracle.analyze_batch(a, oracle.make_params(L, q, rmin, rmax_c, mode), n, sample_bits=16)
+        compare_with_oracle(out, ora, [n] * 8)
+
+
+def test_device_pypow2_and_floor_log2_match_libm(az):
+    import ctypes as C
+    rnd = random.Random(3)
+    xs = [rnd.uniform(-1, 1) for _ in range(200000)]
+    xs += [math.ldexp(rnd.uniform(0.5, 1), rnd.randint(-1074, 1023)) for _ in range(100000)]
+    xs += [0.0, -0.0, 1.0, -1.0, math.inf, 5e-324, 1e154, 1.3407807929942596e154, 1e200, 2.0 ** -600]
+    x = np.array(xs, dtype=np.float64)
+    got = np.zeros_like(x)
+    st = np.zeros(len(x), dtype=np.int32)
+    lib = az.lib
+    rc = lib.flacmi_device_selftest(az.ctx, 0, x.ctypes.data, got.ctypes.data, st.ctypes.data, len(x))
+    assert rc == 0
+    for i in range(0, len(x), 97):
+        want, wst = oracle.pypow2(float(x[i]))
+        assert got[i] == want or (math.isnan(got[i]) and math.isnan(want)), (x[i].hex(), got[i], want)
+        assert st[i] == wst
+    # full corpus against the host emulation (itself checked against libm in test_pymath)
+    hst = C.c_int32()
+    host = np.array([lib.flacmi_host_pypow2(float(v), hst) for v in x])
+    assert np.array_equal(host.view(np.uint64), got.view(np.uint64))
+    pos = np.abs(x[np.isfinite(x) & (x != 0)])
+    got2 = np.zeros_like(pos)
+    st2 = np.zeros(len(pos), dtype=np.int32)
+    assert lib.flacmi_device_selftest(az.ctx, 1, pos.ctypes.data, got2.ctypes.data, st2.ctypes.data, len(pos)) == 0
+    for i in range(0, len(pos), 53):
+        assert int(got2[i]) == oracle.floor_log2(float(pos[i]))[0]
+
+
+def test_synth_device_matches_oracle(az):
+    import ctypes as C
+    n_units, n = 9, 4608
+    for bits, dt in ((16, np.int16), (24, np.int32)):
+        nbytes = np.dtype(dt).itemsize
+        d = az.lib.flacmi_device_alloc(az.ctx, n_units * n * nbytes)
+        az.synth_device(d, nbytes, bits, n, 5, n_units, n, 42)
+        host = np.zeros((n_units, n), dtype=dt)
+        assert az.lib.flacmi_memcpy_d2h(az.ctx, host.ctypes.data, d, host.nbytes) == 0
+        az.lib.flacmi_device_free(az.ctx, d)
+        want = oracle.synth_batch(5, n_units, n, bits, 42, dtype=dt)
+        assert np.array_equal(host, want)
