@@ -1,0 +1,245 @@
+"""Encode-analysis throughput on MI355X (BASELINE.json metric, config 2 workload).
+
+One step = the whole analysis hot path (fixed predictors, Tukey-windowed
+autocorrelation, Levinson-Durbin, LPC quantisation, all candidate residuals, subframe
+choice, Rice partition search; residuals written back zig-zagged for the host packer)
+over one resident batch of --units synthetic 4608-sample int16 blocks per GPU, plus the
+per-step stream statistics that are all-reduced over RCCL when N > 1.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--units U] [--config c2|c3|c5]
+
+For N > 1 the driver starts one process per GPU with torch.distributed.run; each rank
+analyses its own shard (weak scaling: --units per GPU).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    # BASELINE.json configs[1] — the metric's workload
+    "c2": dict(workload="1e6 synthetic mono 4608-sample int16 blocks, -l 12 -q 5 -r 0,5",
+               n=4608, bits=16, L=12, q=5, rmin=0, rmax=5, mode=0, units=1_000_000, channels=1),
+    # configs[2]: stereo 24-bit/96 kHz, -b 16384 -l 32 -q 15 -r 0,8 (each channel one unit)
+    "c3": dict(workload="stereo 24-bit 16384-sample blocks, -l 32 -q 15 -r 0,8",
+               n=16384, bits=24, L=32, q=15, rmin=0, rmax=8, mode=0, units=100_000, channels=2),
+    # configs[4]: fixed-only (-l 0 mode of this build) + Rice search
+    "c5": dict(workload="fixed-only 4608-sample int16 blocks, -r 0,5",
+               n=4608, bits=16, L=0, q=5, rmin=0, rmax=5, mode=1, units=1_000_000, channels=1),
+}
+METRIC = "PCM samples/sec encode-analysis, 4608-blk/16-bit mono, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--units", type=int, default=0, help="units per GPU (default: the config's)")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--parity-units", type=int, default=64)
+    ap.add_argument("--no-parity", action="store_true")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(cfg, meta_np, n_units):
+    """Bytes the analysis must move per batch: samples in, zig-zag residuals (4 B) +
+    per-unit results (meta, Rice parameters) out; the k_lpc -> k_resid LPC record
+    crosses HBM too.  Per kernel:
+      k_lpc  : n*s_in (samples) + 4*rec_words (record)
+      k_resid: n*s_in + 4*rec_words + 4*(n - order) + 208 (meta) + 4*n_parts"""
+    s_in = 2 if cfg["bits"] <= 16 else 4
+    n = cfg["n"]
+    rec = 4 * (2 + cfg["L"] + cfg["L"] * (cfg["L"] + 1) // 2) if cfg["mode"] == 0 else 0
+    res = 4.0 * float(meta_np["res_len"].mean())
+    parts = 4.0 * float(meta_np["n_parts"].mean())
+    lpc = n_units * (n * s_in + rec)
+    resid = n_units * (n * s_in + rec + res + 208 + parts)
+    pipeline = n_units * (n * s_in + res + 208 + parts)
+    return lpc, resid, pipeline
+
+
+def cpu_baseline(cfg, seconds, seed):
+    """Oracle (oracle/flac_oracle.c, a C port of the reference's hot path) on host cores,
+    on a bounded sample of the same workload; chunks of distinct synthetic units."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    threads = min(16, os.cpu_count() or 1)
+    dt = np.int16 if cfg["bits"] <= 16 else np.int32
+    p = oracle.make_params(cfg["L"], cfg["q"], cfg["rmin"], cfg["rmax"], cfg["mode"])
+    chunk = 1024 if cfg["n"] <= 8192 else 128
+    done, t_an, first = 0, 0.0, 0
+    while t_an < seconds:
+        a = oracle.synth_batch(first, chunk, cfg["n"], cfg["bits"], seed, dtype=dt)
+        t0 = time.perf_counter()
+        oracle.analyze_batch(a, p, cfg["n"], sample_bits=cfg["bits"], threads=threads)
+        t_an += time.perf_counter() - t0
+        done += chunk
+        first += chunk
+    return {"value": done * cfg["n"] / t_an, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{done} units x {cfg['n']} samples (synthetic units 0..{done - 1}), "
+                      f"oracle/flac_oracle.c on {threads} host threads, {t_an:.1f} s; the reference "
+                      f"Python itself measured 56.8k samples/s/core here (BASELINE.md)"}
+
+
+def main():
+    args = parse()
+    cfg = dict(CONFIGS[args.config])
+    units = args.units or cfg["units"]
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from flac_amd import abi
+    from flac_amd.analysis import Analyzer, make_params, params_stride_for
+
+    az = Analyzer(local)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    n, bits = cfg["n"], cfg["bits"]
+    sdt = torch.int16 if bits <= 16 else torch.int32
+    sbytes = 2 if bits <= 16 else 4
+    sstride = ((n * sbytes + 15) // 16) * 16 // sbytes
+    rstride = ((n * 4 + 15) // 16) * 16 // 4
+    pstride = params_stride_for(cfg["rmax"])
+    first_unit = rank * units  # contiguous shard of the global unit space (units are independent)
+
+    samples = torch.empty((units, sstride), dtype=sdt, device=dev)
+    meta = torch.empty((units, abi.META_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    rparams = torch.empty((units, pstride), dtype=torch.int32, device=dev)
+    residual = torch.empty((units, rstride), dtype=torch.int32, device=dev)
+    stats = torch.zeros(abi.STATS_WORDS, dtype=torch.int64, device=dev)
+    az.synth_device(samples.data_ptr(), sbytes, bits, sstride, first_unit, units, n, args.seed, sptr)
+    params = make_params(cfg["L"], cfg["q"], cfg["rmin"], cfg["rmax"], cfg["mode"])
+
+    def step():
+        az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, units, n, params, meta.data_ptr(),
+                          rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, sptr)
+        az.stream_stats(meta.data_ptr(), units, n, stats.data_ptr(), sptr)
+        if distributed:
+            dist.all_reduce(stats)  # RCCL over xGMI: the only collective (stream totals)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    az.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kt = az.timing()
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    meta_np = meta.cpu().numpy().view(abi.META_DTYPE).reshape(units)
+    st = stats.cpu().numpy()
+    total_samples = world * units * n * args.steps
+    value = total_samples / elapsed
+
+    # ---- parity: sampled units vs the CPU oracle (outside the timed region) ----
+    parity = None
+    if rank == 0 and not args.no_parity and args.parity_units > 0:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # checker only
+        rng = np.random.default_rng(args.seed)
+        pick = np.sort(rng.choice(units, size=min(args.parity_units, units), replace=False))
+        s_host = samples[torch.as_tensor(pick, device=dev)].cpu().numpy()[:, :n]
+        ora = oracle.analyze_batch(np.ascontiguousarray(s_host), oracle.make_params(cfg["L"], cfg["q"], cfg["rmin"],
+                                   cfg["rmax"], cfg["mode"]), n, sample_bits=bits, threads=16)
+        res_host = residual[torch.as_tensor(pick, device=dev)].cpu().numpy().view(np.uint32)
+        par_host = rparams[torch.as_tensor(pick, device=dev)].cpu().numpy()
+        bad = 0
+        for j, u in enumerate(pick):
+            g, o = meta_np[u], ora["meta"][j]
+            same = all(g[f] == o[f] for f in abi.META_DTYPE.names if f != "coefs") and \
+                np.array_equal(g["coefs"], o["coefs"])
+            off, ln = int(o["res_offset"]), int(o["res_len"])
+            same = same and np.array_equal(res_host[j][off:off + ln].astype(np.uint64), ora["residual"][j][off:off + ln])
+            k = int(o["n_parts"])
+            same = same and np.array_equal(par_host[j][:k], ora["rice_params"][j][:k])
+            bad += 0 if same else 1
+        parity = {"units_checked": int(len(pick)), "mismatches": bad,
+                  "check": "meta, coefficients, zig-zag residual and Rice parameters bit-exact vs oracle"}
+
+    lpc_b, resid_b, pipe_b = algorithmic_bytes(cfg, meta_np, units)
+    lpc_gbs = lpc_b / (kt["lpc_ms"] * 1e-3) / 1e9 if kt["lpc_ms"] > 0 else 0.0
+    resid_gbs = resid_b / (kt["resid_ms"] * 1e-3) / 1e9 if kt["resid_ms"] > 0 else 0.0
+    dominant = "k_resid" if kt["resid_ms"] >= kt["lpc_ms"] else "k_lpc"
+    dom_gbs = resid_gbs if dominant == "k_resid" else lpc_gbs
+    dom_bytes = resid_b if dominant == "k_resid" else lpc_b
+    traffic = None
+    tfile = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tfile):  # HBM bytes per launch from the separate rocprofv3 --pmc passes
+        try:
+            traffic = json.load(open(tfile)).get(dominant)
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = cpu_baseline(cfg, args.cpu_seconds, args.seed) if (world == 1 and args.cpu_seconds > 0) else None
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "i16 in; f64 autocorrelation/Levinson; i32 predictors",
+            "data": "synthetic: on-device integer generator (3 DDS tones + splitmix64 noise, SURVEY §8d)",
+            "config": {"workload": cfg["workload"], "units_per_gpu": units, "block": n, "sample_bits": bits,
+                       "max_lpc_order": cfg["L"], "qlp_precision": cfg["q"], "rice": [cfg["rmin"], cfg["rmax"]],
+                       "mode": "fixed-only" if cfg["mode"] else "reference", "parallelism": f"dp{world} (block shards)"},
+            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": dom_gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": dom_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": dom_bytes},
+            "kernels": {"k_lpc_ms": kt["lpc_ms"], "k_resid_ms": kt["resid_ms"], "call_ms": kt["call_ms"],
+                        "k_lpc_GBs": lpc_gbs, "k_resid_GBs": resid_gbs,
+                        "pipeline_GBs": pipe_b / (kt["call_ms"] * 1e-3) / 1e9 if kt["call_ms"] else 0.0,
+                        "timed_calls": kt["calls"]},
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "stream_stats": {"units": int(st[0]), "samples": int(st[1]), "rice_bits": int(st[2]),
+                             "fixed": int(st[3]), "lpc": int(st[4]), "errors": int(st[65:80].sum())},
+        }
+        print(json.dumps(line), flush=True)
+    az.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -154,6 +154,7 @@ SIGNATURES = {
     "flacmi_memcpy_d2h": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     "flacmi_synchronize": (C.c_int, [C.c_void_p]),
     "flacmi_last_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int]),
+    "flacmi_timing_reset": (C.c_int, [C.c_void_p]),
     "flacmi_host_pypow2": (C.c_double, [C.c_double, C.POINTER(C.c_int32)]),
     "flacmi_host_floor_log2": (C.c_int32, [C.c_double]),
     "flacmi_device_selftest": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,

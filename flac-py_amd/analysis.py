@@ -124,12 +124,17 @@ class Analyzer:
         check(self.lib.flacmi_analyze_device(self.ctx, C.byref(b), C.byref(params), C.byref(o), stream),
               "flacmi_analyze_device")
 
-    def last_timing(self):
-        ms = (C.c_float * 3)()
-        k = self.lib.flacmi_last_timing(self.ctx, ms, 3)
+    def timing(self) -> dict:
+        """Average k_lpc / k_resid / whole-call milliseconds over the analyze calls since
+        the last timing_reset() (HIP events recorded on each call's stream)."""
+        ms = (C.c_float * 4)()
+        k = self.lib.flacmi_last_timing(self.ctx, ms, 4)
         if k < 0:
             check(k, "flacmi_last_timing")
-        return list(ms)[:k]
+        return {"lpc_ms": ms[0], "resid_ms": ms[1], "call_ms": ms[2], "calls": int(ms[3])}
+
+    def timing_reset(self) -> None:
+        check(self.lib.flacmi_timing_reset(self.ctx), "flacmi_timing_reset")
 
     def synth_device(self, dst_ptr: int, sample_bytes: int, sample_bits: int, unit_stride: int,
                      first_unit: int, n_units: int, length: int, seed: int, stream: int = 0) -> None:

@@ -121,9 +121,9 @@ struct flacmi_ctx {
     int32_t* d_sintab = nullptr;
     std::map<int, double*> windows;
     DevBuf rec, h_samples, h_meta, h_params, h_residual, h_acf, h_fs, h_ls, h_recs;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    float last_ms[3] = {0, 0, 0};
-    bool timing_valid = false;
+    static constexpr int kRing = 256;
+    hipEvent_t ev[kRing][3] = {};
+    int ncalls = 0; /* calls since the last timing reset */
 };
 
 static int ensure_buf(DevBuf& b, size_t bytes) {
@@ -179,8 +179,9 @@ flacmi_ctx* flacmi_create(int device) {
     hipError_t e;
     if ((e = hipSetDevice(device)) != hipSuccess) return bad(e, "hipSetDevice");
     if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
-    for (auto& ev : ctx->ev)
-        if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
+    for (auto& slot : ctx->ev)
+        for (auto& ev : slot)
+            if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipMalloc(&ctx->d_log2thr, sizeof(double) * PYM_LOG2_THR_N)) != hipSuccess) return bad(e, "hipMalloc");
     if ((e = hipMemcpy(ctx->d_log2thr, g_log2thr.data(), sizeof(double) * PYM_LOG2_THR_N, hipMemcpyHostToDevice)) != hipSuccess)
         return bad(e, "hipMemcpy");
@@ -200,8 +201,9 @@ void flacmi_destroy(flacmi_ctx* ctx) {
         if (b->p) (void)hipFree(b->p);
     if (ctx->d_log2thr) (void)hipFree(ctx->d_log2thr);
     if (ctx->d_sintab) (void)hipFree(ctx->d_sintab);
-    for (auto& ev : ctx->ev)
-        if (ev) (void)hipEventDestroy(ev);
+    for (auto& slot : ctx->ev)
+        for (auto& ev : slot)
+            if (ev) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -305,7 +307,8 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
     }
     if (o->acf && p->mode != FLACMI_MODE_REFERENCE)
         HIP_TRY(hipMemsetAsync(o->acf, 0, sizeof(double) * 33 * b->n_units, s));
-    HIP_TRY(hipEventRecord(ctx->ev[0], s));
+    hipEvent_t* ev = ctx->ev[ctx->ncalls % flacmi_ctx::kRing];
+    HIP_TRY(hipEventRecord(ev[0], s));
     /* LPC analysis for every class first, then the residual pass */
     for (int c = 0; c < ncls && p->mode == FLACMI_MODE_REFERENCE; ++c) {
         LpcArgs a{};
@@ -324,7 +327,7 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.acf = o->acf ? o->acf + cls[c].unit0 * 33 : nullptr;
         HIP_TRY(launch_lpc(a, s));
     }
-    HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    HIP_TRY(hipEventRecord(ev[1], s));
     for (int c = 0; c < ncls; ++c) {
         ResidArgs a{};
         a.samples = b->samples;
@@ -349,7 +352,8 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.lpc_sums = o->lpc_sums ? o->lpc_sums + cls[c].unit0 * 32 : nullptr;
         HIP_TRY(launch_resid(a, wide, o->residual_bytes, s));
     }
-    HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    HIP_TRY(hipEventRecord(ev[2], s));
+    ctx->ncalls++;
     if (o->lpc_records) {
         if (p->mode == FLACMI_MODE_REFERENCE) {
             HIP_TRY(launch_expand_records((const int32_t*)ctx->rec.p, rec_words, L, b->n_units, o->lpc_records, s));
@@ -357,7 +361,6 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
             HIP_TRY(hipMemsetAsync(o->lpc_records, 0, sizeof(int32_t) * FLACMI_LPC_REC_WORDS(32) * b->n_units, s));
         }
     }
-    ctx->timing_valid = true;
     return 0;
 }
 
@@ -494,16 +497,31 @@ int flacmi_synchronize(flacmi_ctx* ctx) {
 }
 
 int flacmi_last_timing(flacmi_ctx* ctx, float* ms, int n) {
-    if (!ctx || !ctx->timing_valid) return fail(FLACMI_E_INVALID, "no timed call");
+    if (!ctx || ctx->ncalls == 0) return fail(FLACMI_E_INVALID, "no timed call");
     if (int rc = set_device(ctx)) return rc;
-    HIP_TRY(hipEventSynchronize(ctx->ev[2]));
-    float t[3];
-    HIP_TRY(hipEventElapsedTime(&t[0], ctx->ev[0], ctx->ev[1]));
-    HIP_TRY(hipEventElapsedTime(&t[1], ctx->ev[1], ctx->ev[2]));
-    HIP_TRY(hipEventElapsedTime(&t[2], ctx->ev[0], ctx->ev[2]));
-    int k = n < 3 ? n : 3;
-    for (int i = 0; i < k; ++i) ms[i] = t[i];
-    return k;
+    const int k = ctx->ncalls < flacmi_ctx::kRing ? ctx->ncalls : flacmi_ctx::kRing;
+    double acc[3] = {0, 0, 0};
+    for (int c = ctx->ncalls - k; c < ctx->ncalls; ++c) {
+        hipEvent_t* ev = ctx->ev[c % flacmi_ctx::kRing];
+        HIP_TRY(hipEventSynchronize(ev[2]));
+        float t;
+        HIP_TRY(hipEventElapsedTime(&t, ev[0], ev[1]));
+        acc[0] += t;
+        HIP_TRY(hipEventElapsedTime(&t, ev[1], ev[2]));
+        acc[1] += t;
+        HIP_TRY(hipEventElapsedTime(&t, ev[0], ev[2]));
+        acc[2] += t;
+    }
+    const float vals[4] = {(float)(acc[0] / k), (float)(acc[1] / k), (float)(acc[2] / k), (float)k};
+    const int m = n < 4 ? n : 4;
+    for (int i = 0; i < m; ++i) ms[i] = vals[i];
+    return m;
+}
+
+int flacmi_timing_reset(flacmi_ctx* ctx) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    ctx->ncalls = 0;
+    return 0;
 }
 
 double flacmi_host_pypow2(double x, int32_t* status) {

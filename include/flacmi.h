@@ -201,9 +201,13 @@ int flacmi_memcpy_h2d(flacmi_ctx* ctx, void* dst, const void* src, size_t bytes)
 int flacmi_memcpy_d2h(flacmi_ctx* ctx, void* dst, const void* src, size_t bytes);
 int flacmi_synchronize(flacmi_ctx* ctx);
 
-/* ---- timing of the last flacmi_analyze_* call's kernels (HIP events on its stream) ---- */
-/* ms[0] acf+levinson kernels, ms[1] residual+rice kernels, ms[2] whole call; returns count */
+/* ---- kernel timing (HIP events recorded on the stream each analyze call runs on) ----- */
+/* Averages over the analyze calls since the last flacmi_timing_reset (up to 256 calls):
+ * ms[0] k_lpc phase (autocorrelation + Levinson + quantisation), ms[1] k_resid phase
+ * (residual sums + choice + Rice), ms[2] whole call, ms[3] number of calls averaged.
+ * Synchronises on the recorded events; returns the number of values written. */
 int flacmi_last_timing(flacmi_ctx* ctx, float* ms, int n);
+int flacmi_timing_reset(flacmi_ctx* ctx);
 
 /* ---- host-side views of the device arithmetic (for CPU verification of the helpers) ---- */
 /* Python float `x ** 2` as CPython 3.10 + glibc 2.35 pow (FMA variant) computes it;
