@@ -79,14 +79,38 @@ __device__ __forceinline__ double pow2_exact(int e) { /* 2^e, 0 <= e <= 62 */
  * k_resid: fixed + LPC candidate residual sums, choice, chosen residual, Rice search
  * ==================================================================================== */
 
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+/* ---- wave reductions on DPP (VALU lane moves; no LDS traffic) ------------------------
+ * quad_perm [1,0,3,2] and [2,3,0,1], row_half_mirror, row_mirror: every lane ends with its
+ * 16-lane row's sum; row_bcast15 / row_bcast31 then fold the rows so lane 63 holds the
+ * wave total, which readlane broadcasts. */
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_add_u64(uint64_t v) {
+    const uint32_t lo = dpp_u32<CTRL, ROW_MASK>((uint32_t)v);
+    const uint32_t hi = dpp_u32<CTRL, ROW_MASK>((uint32_t)(v >> 32));
+    return v + (((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+    v = dpp_add_u64<0xB1, 0xf>(v);  /* quad_perm [1,0,3,2] */
+    v = dpp_add_u64<0x4E, 0xf>(v);  /* quad_perm [2,3,0,1] */
+    v = dpp_add_u64<0x141, 0xf>(v); /* row_half_mirror */
+    v = dpp_add_u64<0x140, 0xf>(v); /* row_mirror */
+    v = dpp_add_u64<0x142, 0xa>(v); /* row_bcast15 */
+    v = dpp_add_u64<0x143, 0xc>(v); /* row_bcast31 */
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ uint32_t uabs32(int32_t v) { return v < 0 ? (uint32_t)(-v) : (uint32_t)v; }
+/* |a - b| + c on biased (x ^ 0x80000000) operands: one v_sad_u32. */
+__device__ __forceinline__ uint32_t sad_acc(uint32_t a, uint32_t b, uint32_t c) {
+    return (a > b ? a - b : b - a) + c;
+}
+constexpr uint32_t kBias = 0x80000000u;
+
 __device__ __forceinline__ uint64_t uabs64(int64_t v) { return v < 0 ? (uint64_t)(-v) : (uint64_t)v; }
 
 struct Decision {
@@ -120,31 +144,48 @@ __device__ __forceinline__ void put_meta(flacmi_unit_meta* m, int status, int si
     for (int j = 0; j < FLACMI_MAX_LPC_ORDER; ++j) m->coefs[j] = (with_choice && j < d->ncoefs) ? d->coef[j] : 0;
 }
 
-
-template <int LMAX>
-struct ResidLayout {
-    static constexpr int HP = (LMAX > 4 ? ((LMAX + 7) / 8) * 8 : 8); /* history pad */
-    static constexpr int NSUM = 5 + LMAX;
-    static constexpr int CPAD = LMAX > 0 ? ((LMAX + 3) / 4) * 4 : 4; /* coefs per order, padded */
-};
-
-static inline size_t resid_lds_bytes(int lmax, int n, int nw, int P, int xbytes) {
-    const int HP = lmax > 4 ? ((lmax + 7) / 8) * 8 : 8;
-    const int nsum = 5 + lmax;
-    const int cpad = lmax > 0 ? ((lmax + 3) / 4) * 4 : 4;
-    const int npad = ((n + 7) / 8) * 8 + 8;
-    size_t b = (size_t)xbytes * (HP + npad);
-    b = (b + 15) & ~(size_t)15;
-    b += 8 * (size_t)nw * nsum + 8 * (size_t)nsum;
-    b += 4 * (size_t)(lmax > 0 ? lmax : 1) * cpad + 4 * 2 * (size_t)(lmax > 0 ? lmax : 1);
-    b = (b + 15) & ~(size_t)15;
-    b += sizeof(Decision);
-    b = (b + 15) & ~(size_t)15;
-    b += 8 * 32 + 4 * 4;
-    b = (b + 15) & ~(size_t)15;
-    b += 8 * (size_t)(2 * P) + 4 * (size_t)(2 * P);
-    return b;
+/* Workgroup size of k_resid for n samples: 8-sample chunks, up to kCPT per thread while
+ * the workgroup stays <= 256 threads (the kernel's launch bound), more beyond that. */
+__host__ __device__ inline int resid_threads(int n) {
+    const int nch = (n + 7) / 8;
+    int nt = 64 * ((nch + 64 * kCPT - 1) / (64 * kCPT));
+    if (nt > 256) nt = 256;
+    return nt < 64 ? 64 : nt;
+}
+/* samples one thread of k_resid accumulates */
+__host__ __device__ inline int resid_samples_per_thread(int n) {
+    const int nch = (n + 7) / 8;
+    const int nt = resid_threads(n);
+    return 8 * ((nch + nt - 1) / nt);
 }
 
+/* History pad in front of the staged samples (>= LMAX and >= 4, multiple of 8). */
+__host__ __device__ constexpr int resid_hp(int lmax) { return lmax > 4 ? ((lmax + 7) / 8) * 8 : 8; }
+
+/* LDS layout of k_resid: byte offsets (multiples of 16) from the dynamic LDS base.  The
+ * host sizes the allocation with the same function the kernel carves it with. */
+struct ResidLds {
+    int xs, zz, coef, red, tot, dec, rb, misc, hs, hp, total;
+};
+__host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, int P, int xbytes, int zbytes,
+                                                     int coef_bytes) {
+    auto up = [](int b) { return (b + 15) & ~15; };
+    const int nsum = 5 + lmax;
+    const int npad = ((n + 7) / 8) * 8 + 8;
+    ResidLds l;
+    int o = 0;
+    l.xs = o;   o = up(o + xbytes * (resid_hp(lmax) + npad));
+    l.zz = o;   o = up(o + zbytes * npad);
+    l.coef = o; o = up(o + coef_bytes);
+    l.red = o;  o = up(o + 8 * nw * nsum);
+    l.tot = o;  o = up(o + 8 * nsum);
+    l.dec = o;  o = up(o + (int)sizeof(Decision));
+    l.rb = o;   o = up(o + 8 * 32);
+    l.misc = o; o = up(o + 4 * 4);
+    l.hs = o;   o = up(o + 8 * 2 * P);
+    l.hp = o;   o = up(o + 4 * 2 * P);
+    l.total = o;
+    return l;
+}
 
 }  // namespace flacmi

@@ -26,6 +26,7 @@
 #include "../../include/flacmi.h"
 #include "flacmi_kernels.h"
 #include "pymath.h"
+#include "device_common.h"
 
 using namespace flacmi;
 
@@ -274,13 +275,23 @@ static int validate(const flacmi_batch* b, const flacmi_params* p, const flacmi_
     return 0;
 }
 
-/* int32 arithmetic is exact when every |prediction| and |residual| < 2^29 (so an 8-sample
- * partial sum of |r| also fits 32 bits); otherwise the kernels use int64. */
-static bool needs_wide(int bits, int L, int q, int mode) {
+/* int32 arithmetic is exact when every |prediction| and |residual| < 2^26 and a thread's
+ * partial sum of |r| over the samples it owns still fits 32 bits.  Otherwise int64. */
+static bool needs_wide(int n, int bits, int L, int q, int mode) {
     if (bits > 24 || q > 24) return true;
     const double xmax = ldexp(1.0, bits - 1);
     const double rmax = mode == FLACMI_MODE_FIXED_ONLY ? 16.0 * xmax : xmax * (1.0 + (double)L * ldexp(1.0, q - 1)) + 16.0 * xmax;
-    return rmax >= ldexp(1.0, 29);
+    return rmax >= ldexp(1.0, 26) || rmax * resid_samples_per_thread(n) >= ldexp(1.0, 32);
+}
+
+/* FLACMI_DEBUG_STOP=k truncates k_resid after phase k (profiling ablation only: the
+ * outputs are then incomplete). */
+static int debug_stop() {
+    static const int v = [] {
+        const char* e = getenv("FLACMI_DEBUG_STOP");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
 }
 
 static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi_params* p,
@@ -288,7 +299,6 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
     if (int rc = set_device(ctx)) return rc;
     const int L = p->mode == FLACMI_MODE_FIXED_ONLY ? 0 : p->max_lpc_order;
     const int rec_words = FLACMI_LPC_REC_WORDS(L);
-    const bool wide = needs_wide(b->sample_bits, L, p->qlp_precision, p->mode);
     if (p->mode == FLACMI_MODE_REFERENCE) {
         if (int rc = ensure_buf(ctx->rec, sizeof(int32_t) * (size_t)rec_words * (size_t)(b->n_units > 0 ? b->n_units : 1)))
             return rc;
@@ -350,7 +360,10 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.residual_stride = o->residual_stride;
         a.fixed_sums = o->fixed_sums ? o->fixed_sums + cls[c].unit0 * 5 : nullptr;
         a.lpc_sums = o->lpc_sums ? o->lpc_sums + cls[c].unit0 * 32 : nullptr;
-        HIP_TRY(launch_resid(a, wide, o->residual_bytes, s));
+        a.stop_after = debug_stop();
+        const bool wide = needs_wide(cls[c].n, b->sample_bits, L, p->qlp_precision, p->mode);
+        const int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
+        HIP_TRY(launch_resid(a, path, o->residual_bytes, s));
     }
     HIP_TRY(hipEventRecord(ev[2], s));
     ctx->ncalls++;

@@ -41,6 +41,9 @@ struct ResidArgs {
     int64_t residual_stride;
     int64_t* fixed_sums;     /* optional [count][5] */
     int64_t* lpc_sums;       /* optional [count][32] */
+    int32_t stop_after;      /* profiling ablation (env FLACMI_DEBUG_STOP): 0 = full kernel,
+                                1 = after staging, 2 = after candidate sums, 3 = after the
+                                choice, 4 = after the chosen residual */
 };
 
 struct ResidLaunch {
@@ -54,7 +57,8 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes);
 constexpr int kMaxFinestParts = 4096;
 
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);
-hipError_t launch_resid(const ResidArgs& a, bool wide, int residual_bytes, hipStream_t s);
+/* path: 0 = int16 samples / sdot2, 1 = int32 samples / mad24, 2 = int64 arithmetic */
+hipError_t launch_resid(const ResidArgs& a, int path, int residual_bytes, hipStream_t s);
 hipError_t launch_expand_records(const int32_t* rec, int32_t rec_words, int32_t L, int64_t count,
                                  int32_t* out, hipStream_t s);
 hipError_t launch_synth(void* dst, int32_t sample_bytes, int32_t bits, int64_t stride,

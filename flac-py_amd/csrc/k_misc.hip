@@ -4,11 +4,11 @@
 
 namespace flacmi {
 
-hipError_t launch_resid_l0(const ResidArgs&, bool, int, hipStream_t);
-hipError_t launch_resid_l8(const ResidArgs&, bool, int, hipStream_t);
-hipError_t launch_resid_l12(const ResidArgs&, bool, int, hipStream_t);
-hipError_t launch_resid_l16(const ResidArgs&, bool, int, hipStream_t);
-hipError_t launch_resid_l32(const ResidArgs&, bool, int, hipStream_t);
+hipError_t launch_resid_l0(const ResidArgs&, int, int, hipStream_t);
+hipError_t launch_resid_l8(const ResidArgs&, int, int, hipStream_t);
+hipError_t launch_resid_l12(const ResidArgs&, int, int, hipStream_t);
+hipError_t launch_resid_l16(const ResidArgs&, int, int, hipStream_t);
+hipError_t launch_resid_l32(const ResidArgs&, int, int, hipStream_t);
 
 /* ====================================================================================
  * small kernels: record expansion (debug), synthetic PCM, stream statistics
@@ -108,24 +108,22 @@ __global__ __launch_bounds__(256) void k_stats(const flacmi_unit_meta* __restric
 static int lmax_bucket(int L) { return L <= 0 ? 0 : L <= 8 ? 8 : L <= 12 ? 12 : L <= 16 ? 16 : 32; }
 
 ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes) {
-    const int nch = (n + 7) / 8;
-    int nt = 64 * ((nch + 64 * kCPT - 1) / (64 * kCPT));
-    if (nt < 64) nt = 64;
     ResidLaunch r;
-    r.threads = nt;
-    r.lds_bytes = resid_lds_bytes(32, n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff), residual_bytes == 8 ? 8 : 4);
+    r.threads = resid_threads(n);
+    r.lds_bytes = resid_lds_layout(32, n, r.threads / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff), 4,
+                                   residual_bytes == 8 ? 8 : 4, 16 * 1024).total;
     return r;
 }
 
-hipError_t launch_resid(const ResidArgs& a, bool wide, int residual_bytes, hipStream_t s) {
+hipError_t launch_resid(const ResidArgs& a, int path, int residual_bytes, hipStream_t s) {
     if (a.count <= 0) return hipSuccess;
     const int lb = a.mode == FLACMI_MODE_FIXED_ONLY ? 0 : lmax_bucket(a.L);
     switch (lb) {
-        case 0: return launch_resid_l0(a, wide, residual_bytes, s);
-        case 8: return launch_resid_l8(a, wide, residual_bytes, s);
-        case 12: return launch_resid_l12(a, wide, residual_bytes, s);
-        case 16: return launch_resid_l16(a, wide, residual_bytes, s);
-        default: return launch_resid_l32(a, wide, residual_bytes, s);
+        case 0: return launch_resid_l0(a, path, residual_bytes, s);
+        case 8: return launch_resid_l8(a, path, residual_bytes, s);
+        case 12: return launch_resid_l12(a, path, residual_bytes, s);
+        case 16: return launch_resid_l16(a, path, residual_bytes, s);
+        default: return launch_resid_l32(a, path, residual_bytes, s);
     }
 }
 

@@ -1,17 +1,225 @@
 /* k_resid.h — fixed + LPC candidate residual sums, choice, chosen residual and Rice
  * search, one workgroup per unit (see device_common.h for the design notes).
- * Instantiated per LPC-order bucket in k_resid_l*.hip so the builds run in parallel. */
+ * Instantiated per LPC-order bucket in k_resid_l*.hip so the builds run in parallel.
+ *
+ * Three arithmetic paths, chosen on the host from exact magnitude bounds:
+ *   PATH_S16  int16 samples staged in LDS as packed pairs; every LPC prediction is
+ *             ceil(p/2) v_dot2_i32_i16 on (x[i-2-2t], x[i-1-2t]) x (c[2t+1], c[2t]),
+ *             coefficient pairs broadcast from LDS.  |r| sums: one v_sad_u32 each on
+ *             sign-biased operands.  (16-bit samples, q <= 16, |r| < 2^26.)
+ *   PATH_N32  int32 samples, v_mad_i32_i24 predictions (samples and q <= 24 bits).
+ *   PATH_W64  int32 samples, int64 predictions and sums (anything else).
+ * Samples and the zig-zag residual live in separate LDS regions, so the chosen residual
+ * is written to LDS and HBM in the same pass. */
 #pragma once
 #include "device_common.h"
 
 namespace flacmi {
 
-template <int LMAX, bool WIDE, typename ResT>
-__global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) {
-    using Lay = ResidLayout<LMAX>;
-    using X = typename std::conditional<sizeof(ResT) == 8, int64_t, int32_t>::type;
-    using Acc = typename std::conditional<WIDE, int64_t, int32_t>::type;
-    constexpr int HP = Lay::HP, NSUM = Lay::NSUM, CPAD = Lay::CPAD;
+enum { PATH_S16 = 0, PATH_N32 = 1, PATH_W64 = 2 };
+
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int32_t sdot2(uint32_t a, uint32_t b, int32_t c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, a), __builtin_bit_cast(short2v, b), c, false);
+}
+__device__ __forceinline__ int32_t sext24(int32_t v) { return (v << 8) >> 8; }
+
+/* ---------------------------------------------------------------------------------------
+ * PATH_S16: a chunk = 8 samples i0..i0+7 with the HP samples before it, as packed pairs
+ *   E[m] = (x[i0-HP+2m] lo, x[i0-HP+2m+1] hi),  O[m] = (x[i0-HP+2m+1], x[i0-HP+2m+2]).
+ * ------------------------------------------------------------------------------------- */
+template <int HP>
+struct Win16 {
+    static constexpr int NE = (HP + 8) / 2; /* aligned pairs */
+    uint32_t E[NE];
+    uint32_t O[NE - 1];
+    int32_t x[12]; /* samples i0-4 .. i0+7 as int32 */
+    __device__ __forceinline__ void load(const int16_t* xs16, int i0) {
+        const uint4* src = reinterpret_cast<const uint4*>(xs16 + i0 - HP); /* 16-B aligned */
+#pragma unroll
+        for (int g = 0; g < NE / 4; ++g) {
+            const uint4 v = src[g];
+            E[4 * g + 0] = v.x;
+            E[4 * g + 1] = v.y;
+            E[4 * g + 2] = v.z;
+            E[4 * g + 3] = v.w;
+        }
+#pragma unroll
+        for (int m = 0; m < NE - 1; ++m) O[m] = __builtin_amdgcn_alignbit(E[m + 1], E[m], 16);
+#pragma unroll
+        for (int t = 0; t < 12; ++t) {
+            const int pos = HP - 4 + t; /* window position */
+            const uint32_t pr = E[pos >> 1];
+            x[t] = (pos & 1) ? ((int32_t)pr >> 16) : (int32_t)(int16_t)(pr & 0xffff);
+        }
+    }
+    /* pair of taps (2t, 2t+1) for the sample at window position HP + k */
+    __device__ __forceinline__ uint32_t pair(int k, int t) const {
+        const int lo = HP + k - 2 - 2 * t; /* index of x[i-2-2t] */
+        return (lo & 1) ? O[(lo - 1) >> 1] : E[lo >> 1];
+    }
+};
+
+/* fixed orders 0..4 from the 12 samples x[i0-4 .. i0+7] (shared by all paths), with
+ * running differences: per sample 4 subtractions, 4 bias xors and 5 v_sad_u32. */
+template <bool MASKED, typename A>
+__device__ __forceinline__ void fixed_sums32(const int32_t (&x)[12], int i0, int n, A* acc) {
+    /* state after sample i-1: x, D1, D2, D3 (plain and biased) */
+    int32_t xp = x[3];
+    int32_t d1p = x[3] - x[2];
+    int32_t d2p = d1p - (x[2] - x[1]);
+    int32_t d3p = d2p - ((x[2] - x[1]) - (x[1] - x[0]));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t xc = x[4 + k];
+        const int32_t d1 = xc - xp, d2 = d1 - d1p, d3 = d2 - d2p;
+        const uint32_t xb = (uint32_t)xc ^ kBias;
+        uint32_t s0 = sad_acc(xb, kBias, 0);                                        /* |x|  */
+        uint32_t s1 = sad_acc(xb, (uint32_t)xp ^ kBias, 0);                         /* |D1| */
+        uint32_t s2 = sad_acc((uint32_t)d1 ^ kBias, (uint32_t)d1p ^ kBias, 0);      /* |D2| */
+        uint32_t s3 = sad_acc((uint32_t)d2 ^ kBias, (uint32_t)d2p ^ kBias, 0);      /* |D3| */
+        uint32_t s4 = sad_acc((uint32_t)d3 ^ kBias, (uint32_t)d3p ^ kBias, 0);      /* |D4| */
+        if (MASKED) {
+            const int i = i0 + k;
+            const bool in = i < n;
+            s0 = in ? s0 : 0;
+            s1 = (in && i >= 1) ? s1 : 0;
+            s2 = (in && i >= 2) ? s2 : 0;
+            s3 = (in && i >= 3) ? s3 : 0;
+            s4 = (in && i >= 4) ? s4 : 0;
+        }
+        acc[0] += s0;
+        acc[1] += s1;
+        acc[2] += s2;
+        acc[3] += s3;
+        acc[4] += s4;
+        xp = xc;
+        d1p = d1;
+        d2p = d2;
+        d3p = d3;
+    }
+}
+
+/* LDS tables of the LPC candidates, filled in phase A */
+template <int LMAX>
+struct CoefTables {
+    static constexpr int NP = (LMAX + 1) / 2;                       /* pairs per order */
+    static constexpr int PPAD = NP > 0 ? ((NP + 3) / 4) * 4 : 4;    /* padded to uint4 */
+    static constexpr int CPAD = LMAX > 0 ? ((LMAX + 3) / 4) * 4 : 4;
+    static constexpr int BYTES = 16 * ((4 * LMAX * (PPAD + CPAD) + 8 * LMAX + 15) / 16);
+};
+
+template <int LMAX, int HP, bool MASKED>
+__device__ __forceinline__ void chunk_sums_s16(const Win16<HP>& W, int i0, int n, int L, bool do_lpc,
+                                               const uint32_t* cpair, const int32_t* lsh,
+                                               uint32_t (&acc)[5 + LMAX]) {
+    using CT = CoefTables<LMAX>;
+    fixed_sums32<MASKED>(W.x, i0, n, acc);
+    if (!do_lpc) return;
+    static_for<LMAX>([&](auto P_) {
+        constexpr int pp = P_ + 1;
+        constexpr int np = (pp + 1) / 2;
+        __builtin_amdgcn_sched_barrier(0); /* one candidate at a time: bounds register pressure */
+        if (pp <= L) {
+            uint32_t cq[np];
+            const uint4* src = reinterpret_cast<const uint4*>(cpair + (pp - 1) * CT::PPAD);
+#pragma unroll
+            for (int g = 0; g < (np + 3) / 4; ++g) {
+                const uint4 v = src[g];
+                if (4 * g + 0 < np) cq[4 * g + 0] = v.x;
+                if (4 * g + 1 < np) cq[4 * g + 1] = v.y;
+                if (4 * g + 2 < np) cq[4 * g + 2] = v.z;
+                if (4 * g + 3 < np) cq[4 * g + 3] = v.w;
+            }
+            const int sh = lsh[pp - 1];
+            const int start = lsh[LMAX + pp - 1];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                int32_t pred = 0;
+#pragma unroll
+                for (int t = 0; t < np; ++t) pred = sdot2(W.pair(k, t), cq[t], pred);
+                uint32_t s = sad_acc((uint32_t)W.x[4 + k] ^ kBias, (uint32_t)(pred >> sh) ^ kBias, 0);
+                if (MASKED) {
+                    const int i = i0 + k;
+                    s = (i >= start && i < n) ? s : 0;
+                }
+                acc[4 + pp] += s;
+            }
+        }
+    });
+}
+
+/* PATH_N32 / PATH_W64: int32 window of HP + 8 samples */
+template <int LMAX, int HP, bool MASKED, bool WIDE>
+__device__ __forceinline__ void chunk_sums_32(const int32_t (&w)[HP + 8], int i0, int n, int L, bool do_lpc,
+                                              const int32_t* cfl, const int32_t* lsh,
+                                              typename std::conditional<WIDE, uint64_t, uint32_t>::type (&acc)[5 + LMAX]) {
+    using CT = CoefTables<LMAX>;
+    int32_t x12[12];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) x12[t] = w[HP - 4 + t];
+    if constexpr (!WIDE) {
+        fixed_sums32<MASKED>(x12, i0, n, acc);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k;
+            const int64_t x0 = w[HP + k], x1 = w[HP + k - 1], x2 = w[HP + k - 2], x3 = w[HP + k - 3],
+                          x4 = w[HP + k - 4];
+            const int64_t r[5] = {x0, x0 - x1, x0 - 2 * x1 + x2, x0 - 3 * x1 + 3 * x2 - x3,
+                                  x0 - 4 * x1 + 6 * x2 - 4 * x3 + x4};
+#pragma unroll
+            for (int o = 0; o < 5; ++o) acc[o] += (!MASKED || (i >= o && i < n)) ? uabs64(r[o]) : 0;
+        }
+    }
+    if (!do_lpc) return;
+    static_for<LMAX>([&](auto P_) {
+        constexpr int pp = P_ + 1;
+        __builtin_amdgcn_sched_barrier(0); /* one candidate at a time: bounds register pressure */
+        if (pp <= L) {
+            int32_t c[pp];
+            const int4v* src = reinterpret_cast<const int4v*>(cfl + (pp - 1) * CT::CPAD);
+#pragma unroll
+            for (int g = 0; g < (pp + 3) / 4; ++g) {
+                const int4v v = src[g];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (4 * g + e < pp) c[4 * g + e] = v[e];
+            }
+            const int sh = lsh[pp - 1];
+            const int start = lsh[LMAX + pp - 1];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = i0 + k;
+                if constexpr (!WIDE) {
+                    int32_t pred = 0;
+#pragma unroll
+                    for (int j = 0; j < pp; ++j) pred += sext24(c[j]) * sext24(w[HP + k - 1 - j]);
+                    uint32_t s = sad_acc((uint32_t)w[HP + k] ^ kBias, (uint32_t)(pred >> sh) ^ kBias, 0);
+                    if (MASKED) s = (i >= start && i < n) ? s : 0;
+                    acc[4 + pp] += s;
+                } else {
+                    int64_t pred = 0;
+#pragma unroll
+                    for (int j = 0; j < pp; ++j) pred += (int64_t)c[j] * (int64_t)w[HP + k - 1 - j];
+                    const uint64_t v = uabs64((int64_t)w[HP + k] - (pred >> sh));
+                    acc[4 + pp] += (!MASKED || (i >= start && i < n)) ? v : 0;
+                }
+            }
+        }
+    });
+}
+
+template <int LMAX, int PATH, typename ResT>
+__global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
+    using UX = ResT;
+    constexpr bool S16 = PATH == PATH_S16;
+    constexpr bool WIDE = PATH == PATH_W64;
+    using A = typename std::conditional<WIDE, uint64_t, uint32_t>::type; /* per-thread partial */
+    using CT = CoefTables<LMAX>;
+    constexpr int HP = resid_hp(LMAX);
+    constexpr int NSUM = 5 + LMAX;
 
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, wid = tid >> 6, nw = NT >> 6;
@@ -20,73 +228,83 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
     const int n = a.n, L = a.L;
     const int nch = (n + 7) >> 3;
     const int npad = nch * 8 + 8;
+    const bool ref_mode = a.mode == FLACMI_MODE_REFERENCE;
+    const bool do_lpc = LMAX > 0 && ref_mode;
 
-    /* ---- LDS carve ---- */
-    X* xs = reinterpret_cast<X*>(smem) + HP;                                   /* [-HP, npad) */
-    unsigned char* p = smem + sizeof(X) * (size_t)(HP + npad);
-    p = (unsigned char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    unsigned long long* red = reinterpret_cast<unsigned long long*>(p);       /* [nw][NSUM] */
-    p += sizeof(unsigned long long) * nw * NSUM;
-    unsigned long long* tot = reinterpret_cast<unsigned long long*>(p);       /* [NSUM] */
-    p += sizeof(unsigned long long) * NSUM;
-    int32_t* cf = reinterpret_cast<int32_t*>(p);                               /* [LMAX][CPAD] */
-    p += sizeof(int32_t) * (LMAX > 0 ? LMAX : 1) * CPAD;
-    int32_t* lsh = reinterpret_cast<int32_t*>(p);                              /* [LMAX] shift, start */
-    p += sizeof(int32_t) * 2 * (LMAX > 0 ? LMAX : 1);
-    p = (unsigned char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    Decision* dec = reinterpret_cast<Decision*>(p);
-    p += sizeof(Decision);
-    p = (unsigned char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    unsigned long long* rb = reinterpret_cast<unsigned long long*>(p);        /* [16] fixed bits, [16] data bits */
-    p += sizeof(unsigned long long) * 32;
-    int* misc = reinterpret_cast<int*>(p);                                     /* [0] err key, [1] any>14, [2] wide flag */
-    p += sizeof(int) * 4;
-    p = (unsigned char*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
-    unsigned long long* hs = reinterpret_cast<unsigned long long*>(p);        /* heap S [2P] */
-    /* heap params follow hs: set after P is known */
-
+    /* ---- LDS carve (integer offsets keep every access a ds_* instruction) ---- */
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (n % (1 << o) == 0) rmax_eff = o;
+    const ResidLds lay = resid_lds_layout(LMAX, n, nw, 1 << (rmax_eff < 0 ? 0 : rmax_eff), S16 ? 2 : 4,
+                                          (int)sizeof(ResT), CT::BYTES);
+    int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
+    int32_t* xs32 = reinterpret_cast<int32_t*>(smem + lay.xs) + HP; /* [-HP, npad) (others) */
+    ResT* zz = reinterpret_cast<ResT*>(smem + lay.zz);              /* [npad] */
+    uint32_t* cpair = reinterpret_cast<uint32_t*>(smem + lay.coef);  /* [LMAX][PPAD] */
+    int32_t* cfl = reinterpret_cast<int32_t*>(smem + lay.coef + 4 * LMAX * CT::PPAD); /* [LMAX][CPAD] */
+    int32_t* lsh = cfl + LMAX * CT::CPAD;                            /* [2*LMAX] shift, start */
+    unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + lay.red);
+    unsigned long long* tot = reinterpret_cast<unsigned long long*>(smem + lay.tot);
+    Decision* dec = reinterpret_cast<Decision*>(smem + lay.dec);
+    unsigned long long* rb = reinterpret_cast<unsigned long long*>(smem + lay.rb);
+    int* misc = reinterpret_cast<int*>(smem + lay.misc);
+    unsigned long long* hs = reinterpret_cast<unsigned long long*>(smem + lay.hs);
+    int32_t* hp = reinterpret_cast<int32_t*>(smem + lay.hp);
     flacmi_unit_meta* meta = a.meta + gid;
+    const int32_t* __restrict__ rec = ref_mode ? a.rec + gid * a.rec_words : nullptr;
 
-    /* ---- phase A: stage samples, coefficients ---- */
-    for (int i = tid; i < HP; i += NT) xs[i - HP] = 0;
-    for (int i = n + tid; i < npad; i += NT) xs[i] = 0;
-    if (a.sample_bytes == 2) {
-        const int16_t* __restrict__ src = (const int16_t*)a.samples + u * a.stride;
-        const int nv = n >> 3;
-        for (int v = tid; v < nv; v += NT) {
-            const short8 s = *reinterpret_cast<const short8*>(src + 8 * v);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) xs[8 * v + k] = s[k];
-        }
-        for (int i = nv * 8 + tid; i < n; i += NT) xs[i] = src[i];
-    } else {
-        const int32_t* __restrict__ src = (const int32_t*)a.samples + u * a.stride;
-        const int nv = n >> 2;
-        for (int v = tid; v < nv; v += NT) {
-            const int4v s = *reinterpret_cast<const int4v*>(src + 4 * v);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) xs[4 * v + k] = s[k];
-        }
-        for (int i = nv * 4 + tid; i < n; i += NT) xs[i] = src[i];
-    }
-    if (a.mode == FLACMI_MODE_REFERENCE) {
-        const int32_t* __restrict__ rec = a.rec + gid * a.rec_words;
+    /* ---- phase A: stage samples and the candidate coefficients ---- */
+    if (ref_mode) {
         const int st = rec[0];
         if (st != 0) { /* the reference raises inside encode_subframe_lpc */
             if (tid == 0) put_meta(meta, st & 0xffff, st >> 16, nullptr, 0);
             return;
         }
+    }
+    if constexpr (S16) {
+        for (int i = tid; i < HP; i += NT) xs16[i - HP] = 0;
+        for (int i = n + tid; i < npad; i += NT) xs16[i] = 0;
+        const int16_t* __restrict__ src = (const int16_t*)a.samples + u * a.stride;
+        const int nv = n >> 3;
+        for (int v = tid; v < nv; v += NT)
+            *reinterpret_cast<uint4*>(xs16 + 8 * v) = *reinterpret_cast<const uint4*>(src + 8 * v);
+        for (int i = nv * 8 + tid; i < n; i += NT) xs16[i] = src[i];
+    } else {
+        for (int i = tid; i < HP; i += NT) xs32[i - HP] = 0;
+        for (int i = n + tid; i < npad; i += NT) xs32[i] = 0;
+        if (a.sample_bytes == 2) {
+            const int16_t* __restrict__ src = (const int16_t*)a.samples + u * a.stride;
+            const int nv = n >> 3;
+            for (int v = tid; v < nv; v += NT) {
+                const short8 s = *reinterpret_cast<const short8*>(src + 8 * v);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) xs32[8 * v + k] = s[k];
+            }
+            for (int i = nv * 8 + tid; i < n; i += NT) xs32[i] = src[i];
+        } else {
+            const int32_t* __restrict__ src = (const int32_t*)a.samples + u * a.stride;
+            const int nv = n >> 2;
+            for (int v = tid; v < nv; v += NT)
+                *reinterpret_cast<int4v*>(xs32 + 4 * v) = *reinterpret_cast<const int4v*>(src + 4 * v);
+            for (int i = nv * 4 + tid; i < n; i += NT) xs32[i] = src[i];
+        }
+    }
+    if (do_lpc) {
         const uint32_t negmask = (uint32_t)rec[1];
-        for (int i = tid; i < LMAX * CPAD; i += NT) {
-            const int pp = i / CPAD + 1, j = i % CPAD;
-            const bool neg = (negmask >> (pp - 1)) & 1;
-            cf[i] = (pp <= L && j < pp && !neg) ? rec[2 + L + (pp * (pp - 1)) / 2 + j] : 0;
+        for (int i = tid; i < LMAX * CT::CPAD; i += NT) {
+            const int pp = i / CT::CPAD + 1, j = i % CT::CPAD;
+            cfl[i] = (pp <= L && j < pp) ? rec[2 + L + (pp * (pp - 1)) / 2 + j] : 0;
+        }
+        for (int i = tid; i < LMAX * CT::PPAD; i += NT) {
+            const int pp = i / CT::PPAD + 1, t = i % CT::PPAD;
+            const int32_t* cp = rec + 2 + L + (pp * (pp - 1)) / 2;
+            const int32_t hi = (pp <= L && 2 * t < pp) ? cp[2 * t] : 0;
+            const int32_t lo = (pp <= L && 2 * t + 1 < pp) ? cp[2 * t + 1] : 0;
+            cpair[i] = ((uint32_t)hi << 16) | ((uint32_t)lo & 0xffffu);
         }
         for (int i = tid; i < LMAX; i += NT) {
-            const int pp = i + 1;
-            const bool neg = (negmask >> i) & 1;
-            lsh[i] = pp <= L ? rec[2 + i] : 0;
-            lsh[LMAX + i] = neg ? 0 : pp; /* first residual index of this candidate */
+            lsh[i] = i < L ? rec[2 + i] : 0;
+            lsh[LMAX + i] = ((negmask >> i) & 1) ? 0 : i + 1; /* first residual index */
         }
     }
     if (tid == 0) {
@@ -96,78 +314,43 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
     }
     if (tid < 32) rb[tid] = 0;
     __syncthreads();
+    if (a.stop_after == 1) return;
 
     /* ---- phase B: sum|r| for fixed orders 0..4 and LPC orders 1..L ---- */
-    unsigned long long sums[NSUM];
+    A acc[NSUM];
 #pragma unroll
-    for (int s = 0; s < NSUM; ++s) sums[s] = 0;
-    const bool do_lpc = LMAX > 0 && a.mode == FLACMI_MODE_REFERENCE;
+    for (int s = 0; s < NSUM; ++s) acc[s] = 0;
 #pragma unroll 1
     for (int c = tid; c < nch; c += NT) {
-        {
-            const int i0 = 8 * c;
-            X w[HP + 8];
+        const int i0 = 8 * c;
+        const bool fast = (i0 >= HP) && (i0 + 8 <= n);
+        if constexpr (S16) {
+            Win16<HP> W;
+            W.load(xs16, i0);
+            if (fast) chunk_sums_s16<LMAX, HP, false>(W, i0, n, L, do_lpc, cpair, lsh, acc);
+            else chunk_sums_s16<LMAX, HP, true>(W, i0, n, L, do_lpc, cpair, lsh, acc);
+        } else {
+            int32_t w[HP + 8];
+            const int4v* src = reinterpret_cast<const int4v*>(xs32 + i0 - HP);
 #pragma unroll
-            for (int j = 0; j < HP + 8; ++j) w[j] = xs[i0 - HP + j];
-            const bool fast = (i0 >= HP) && (i0 + 8 <= n);
-            /* fixed predictors: k-th differences (FIXED_PREDICTOR_COEFFICIENTS) */
-            uint32_t fp[5] = {0, 0, 0, 0, 0};
-            unsigned long long fpw[5] = {0, 0, 0, 0, 0};
+            for (int g = 0; g < (HP + 8) / 4; ++g) {
+                const int4v v = src[g];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int i = i0 + k;
-                const int64_t x0 = w[HP + k], x1 = w[HP + k - 1], x2 = w[HP + k - 2],
-                              x3 = w[HP + k - 3], x4 = w[HP + k - 4];
-                const int64_t r[5] = {x0, x0 - x1, x0 - 2 * x1 + x2, x0 - 3 * x1 + 3 * x2 - x3,
-                                      x0 - 4 * x1 + 6 * x2 - 4 * x3 + x4};
-#pragma unroll
-                for (int o = 0; o < 5; ++o) {
-                    const bool valid = fast || (i >= o && i < n);
-                    if (WIDE) fpw[o] += valid ? uabs64(r[o]) : 0;
-                    else fp[o] += valid ? uabs32((int32_t)r[o]) : 0;
-                }
+                for (int e = 0; e < 4; ++e) w[4 * g + e] = v[e];
             }
-#pragma unroll
-            for (int o = 0; o < 5; ++o) sums[o] += WIDE ? fpw[o] : fp[o];
-            if (do_lpc) {
-                static_for<LMAX>([&](auto P_) {
-                    constexpr int pp = P_ + 1;
-                    if (pp <= L) {
-                        Acc coef[LMAX > 0 ? LMAX : 1];
-#pragma unroll
-                        for (int j = 0; j < LMAX; ++j)
-                            if (j < pp) coef[j] = cf[(pp - 1) * CPAD + j];
-                        const int sh = lsh[pp - 1];
-                        const int start = lsh[LMAX + pp - 1];
-                        uint32_t part = 0;
-                        unsigned long long partw = 0;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            Acc pred = 0;
-#pragma unroll
-                            for (int j = 0; j < LMAX; ++j) {
-                                if (j < pp) {
-                                    if (WIDE) pred += (Acc)coef[j] * (Acc)w[HP + k - 1 - j];
-                                    else pred += __mul24((int)coef[j], (int)w[HP + k - 1 - j]);
-                                }
-                            }
-                            const Acc r = (Acc)w[HP + k] - (pred >> sh);
-                            const int i = i0 + k;
-                            const bool valid = fast ? (i >= start) : (i >= start && i < n);
-                            if (WIDE) partw += valid ? uabs64(r) : 0;
-                            else part += valid ? uabs32((int32_t)r) : 0;
-                        }
-                        sums[4 + pp] += WIDE ? partw : part;
-                    }
-                });
-            }
+            if (fast) chunk_sums_32<LMAX, HP, false, WIDE>(w, i0, n, L, do_lpc, cfl, lsh, acc);
+            else chunk_sums_32<LMAX, HP, true, WIDE>(w, i0, n, L, do_lpc, cfl, lsh, acc);
         }
     }
 
+    if (a.stop_after == 2) {
+        if (tid == 0) meta->rice_bits = (long long)acc[0] + (long long)acc[NSUM - 1];
+        return;
+    }
     /* ---- phase C: workgroup reduction ---- */
 #pragma unroll
     for (int s = 0; s < NSUM; ++s) {
-        const unsigned long long v = wave_sum(sums[s]);
+        const uint64_t v = wave_sum_u64((uint64_t)acc[s]);
         if (lane == 0) red[wid * NSUM + s] = v;
     }
     __syncthreads();
@@ -195,7 +378,7 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
         d.ncoefs = 0;
         d.lpc_order = 0;
         d.lpc_sum = 0;
-        for (int j = 0; j < 4; ++j) d.coef[j] = c_fixed_coef[fo][j];
+        for (int j = 0; j < FLACMI_MAX_LPC_ORDER; ++j) d.coef[j] = j < 4 ? c_fixed_coef[fo][j] : 0;
         if (do_lpc) {
             int best = 1;
             for (int pp = 2; pp <= L; ++pp)
@@ -203,11 +386,13 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
             d.lpc_order = best;
             d.lpc_sum = (long long)tot[4 + best];
             if (tot[4 + best] < tot[fo]) {
+                /* A coefficient-less candidate (negative-shift branch) sums |x| over all n
+                 * samples, exactly the fixed order-0 sum, so it never gets here. */
                 d.kind = FLACMI_KIND_LPC;
                 d.order = best;
                 d.shift = lsh[best - 1];
-                d.ncoefs = lsh[LMAX + best - 1] == 0 ? 0 : best;
-                for (int j = 0; j < best; ++j) d.coef[j] = cf[(best - 1) * CPAD + j];
+                d.ncoefs = best;
+                for (int j = 0; j < best; ++j) d.coef[j] = cfl[(best - 1) * CT::CPAD + j];
             } else if (!(tot[fo] < tot[4 + best])) {
                 d.status = ST_ASSERT;
                 d.site = FLACMI_SITE_CHOICE_TIE;
@@ -227,71 +412,99 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
         if (tid == 0) put_meta(meta, dstatus, dec->site, dec, 0);
         return;
     }
-    /* The chosen LPC candidate always has coefficients: a coefficient-less candidate
-     * (negative-shift branch) has sum|x| over all n samples, which is exactly the fixed
-     * order-0 sum, so it can never be strictly smaller than the best fixed sum. */
+    if (a.stop_after == 3) return;
     const int order = dec->order;
     const int dshift = dec->shift;
-    const int start = order; /* residual starts at index len(warmup) */
+    const int start = order; /* the residual starts at index len(warmup) */
+    constexpr int TAPS = LMAX > 4 ? LMAX : 4;
 
-    /* ---- phase E: chosen residual, zig-zag, to HBM and (after a barrier) to LDS ---- */
-    ResT zr[kCPT][8];
-    bool wide_flag = false;
+    /* ---- phase E: chosen residual, zig-zag, to LDS and HBM ---- */
+    int wide_flag = 0;
     ResT* __restrict__ rout = reinterpret_cast<ResT*>(a.residual) + gid * a.residual_stride;
-    static_for<kCPT>([&](auto C_) {
-        constexpr int cc = C_;
-        const int c = tid + cc * NT;
-        if (c < nch) {
-            const int i0 = 8 * c;
-            X w[HP + 8];
+    {
+        int32_t cf[TAPS];
 #pragma unroll
-            for (int j = 0; j < HP + 8; ++j) w[j] = xs[i0 - HP + j];
+        for (int j = 0; j < TAPS; ++j) cf[j] = dec->coef[j];
+#pragma unroll 1
+        for (int c = tid; c < nch; c += NT) {
+            const int i0 = 8 * c;
+            int32_t w[HP + 8];
+            if constexpr (S16) {
+                const uint4* src = reinterpret_cast<const uint4*>(xs16 + i0 - HP);
+#pragma unroll
+                for (int g = 0; g < (HP + 8) / 8; ++g) {
+                    const uint4 v = src[g];
+                    const uint32_t q4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        w[8 * g + 2 * e] = (int32_t)(int16_t)(q4[e] & 0xffff);
+                        w[8 * g + 2 * e + 1] = (int32_t)q4[e] >> 16;
+                    }
+                }
+            } else {
+                const int4v* src = reinterpret_cast<const int4v*>(xs32 + i0 - HP);
+#pragma unroll
+                for (int g = 0; g < (HP + 8) / 4; ++g) {
+                    const int4v v = src[g];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w[4 * g + e] = v[e];
+                }
+            }
+            ResT zv[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                int64_t pred = 0;
+                int64_t r;
+                if constexpr (!WIDE) {
+                    int32_t pred = 0;
+                    if (order <= 4) {
 #pragma unroll
-                for (int j = 0; j < (LMAX > 4 ? LMAX : 4); ++j)
-                    if (j < order) pred += (int64_t)dec->coef[j] * (int64_t)w[HP + k - 1 - j];
-                const int64_t r = (int64_t)w[HP + k] - (pred >> dshift);
+                        for (int j = 0; j < 4; ++j) pred += sext24(cf[j]) * sext24(w[HP + k - 1 - j]);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < TAPS; ++j) pred += sext24(cf[j]) * sext24(w[HP + k - 1 - j]);
+                    }
+                    r = (int64_t)(w[HP + k] - (pred >> dshift));
+                } else {
+                    int64_t pred = 0;
+#pragma unroll
+                    for (int j = 0; j < TAPS; ++j) pred += (int64_t)cf[j] * (int64_t)w[HP + k - 1 - j];
+                    r = (int64_t)w[HP + k] - (pred >> dshift);
+                }
                 const int i = i0 + k;
                 ResT z;
-                if (sizeof(ResT) == 4) {
-                    const bool fits = r >= -(1LL << 31) && r < (1LL << 31);
-                    if (!fits && i >= start && i < n) wide_flag = true;
+                if constexpr (sizeof(ResT) == 4) {
+                    if (WIDE && !(r >= -(1LL << 31) && r < (1LL << 31)) && i >= start && i < n) wide_flag = 1;
                     const int32_t r32 = (int32_t)r;
                     z = (ResT)(((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31));
                 } else {
                     z = (ResT)(((uint64_t)r << 1) ^ (uint64_t)(r >> 63));
                 }
-                zr[cc][k] = (i >= start && i < n) ? z : (ResT)0;
+                zv[k] = (i >= start && i < n) ? z : (ResT)0;
             }
-            if (i0 + 8 <= n) {
-                if constexpr (sizeof(ResT) == 4) {
-                    int4v* o = reinterpret_cast<int4v*>(rout + i0);
-                    o[0] = int4v{(int)zr[cc][0], (int)zr[cc][1], (int)zr[cc][2], (int)zr[cc][3]};
-                    o[1] = int4v{(int)zr[cc][4], (int)zr[cc][5], (int)zr[cc][6], (int)zr[cc][7]};
+            if constexpr (sizeof(ResT) == 4) {
+                const uint4 lo{zv[0], zv[1], zv[2], zv[3]}, hi{zv[4], zv[5], zv[6], zv[7]};
+                reinterpret_cast<uint4*>(zz + i0)[0] = lo;
+                reinterpret_cast<uint4*>(zz + i0)[1] = hi;
+                if (i0 + 8 <= n) {
+                    reinterpret_cast<uint4*>(rout + i0)[0] = lo;
+                    reinterpret_cast<uint4*>(rout + i0)[1] = hi;
                 } else {
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) rout[i0 + k] = zr[cc][k];
+                    for (int k = 0; k < 8; ++k)
+                        if (i0 + k < n) rout[i0 + k] = zv[k];
                 }
             } else {
 #pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    if (i0 + k < n) rout[i0 + k] = zr[cc][k];
+                for (int k = 0; k < 8; ++k) {
+                    zz[i0 + k] = zv[k];
+                    if (i0 + k < n) rout[i0 + k] = zv[k];
+                }
             }
         }
-    });
+    }
     if (wide_flag) misc[2] = 1;
     __syncthreads();
-    static_for<kCPT>([&](auto C_) {
-        constexpr int cc = C_;
-        const int c = tid + cc * NT;
-        if (c < nch) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) xs[8 * c + k] = (X)zr[cc][k];
-        }
-    });
-    __syncthreads();
+    if (a.stop_after == 4) return;
     if (misc[2]) {
         if (tid == 0) put_meta(meta, FLACMI_STATUS_RESIDUAL_WIDE, FLACMI_SITE_RESIDUAL_WIDTH, dec, 1);
         return;
@@ -307,13 +520,12 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
     }
     const int rmin = a.rmin;
     const int P = 1 << omax, ps = n >> omax;
-    int32_t* hp = reinterpret_cast<int32_t*>(hs + 2 * P); /* heap params [2P] */
-    /* finest partition sums: heap nodes [P, 2P) */
+    /* finest partition sums: heap nodes [P, 2P); zz[i] = 0 for i < start */
     for (int k = wid; k < P; k += nw) {
-        const int lo = k == 0 ? start : k * ps, hi = (k + 1) * ps;
-        unsigned long long s = 0;
-        for (int i = lo + lane; i < hi; i += 64) s += (unsigned long long)(typename std::make_unsigned<X>::type)xs[i];
-        s = wave_sum(s);
+        const int lo = k * ps, hi = (k + 1) * ps;
+        uint64_t s = 0;
+        for (int i = lo + lane; i < hi; i += 64) s += (uint64_t)zz[i];
+        s = wave_sum_u64(s);
         if (lane == 0) hs[P + k] = s;
     }
     __syncthreads();
@@ -334,12 +546,13 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
         if (S == 0) {
             atomicMin(&misc[0], (o << 16) | K);
         } else {
-            const double mean = (double)S / (double)len; /* S < 2^53: exact division rounding */
+            const double mean = (double)S / (double)len; /* S < 2^53: correctly rounded */
             prm = pym::py_floor_log2(mean, a.log2thr);
             if (prm < 0) atomicMin(&misc[0], (o << 16) | K);
         }
         hp[j] = prm;
-        const unsigned long long hb = 4ull + (prm > 14 ? 5ull : 4ull) + (unsigned long long)len * (unsigned long long)(1 + prm);
+        const unsigned long long hb =
+            4ull + (prm > 14 ? 5ull : 4ull) + (unsigned long long)len * (unsigned long long)(1 + prm);
         atomicAdd(&rb[o], hb);
     }
     __syncthreads();
@@ -353,26 +566,26 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
         return;
     }
     /* data bits: sum over the residual of (x >> p) for every candidate order at once */
-    unsigned long long tb[16];
+    uint64_t tb[16];
 #pragma unroll
     for (int o = 0; o < 16; ++o) tb[o] = 0;
     for (int k = wid; k < P; k += nw) {
         int pk[16];
 #pragma unroll
         for (int o = 0; o < 16; ++o) pk[o] = (o >= rmin && o <= omax) ? hp[(1 << o) + (k >> (omax - o))] : 0;
-        const int lo = k == 0 ? start : k * ps, hi = (k + 1) * ps;
+        const int lo = k * ps, hi = (k + 1) * ps;
         for (int i = lo + lane; i < hi; i += 64) {
-            const auto xv = (typename std::make_unsigned<X>::type)xs[i];
+            const UX xv = zz[i];
 #pragma unroll
             for (int o = 0; o < 16; ++o)
-                if (o >= rmin && o <= omax) tb[o] += (unsigned long long)(xv >> pk[o]);
+                if (o >= rmin && o <= omax) tb[o] += (uint64_t)(xv >> pk[o]);
         }
     }
 #pragma unroll
     for (int o = 0; o < 16; ++o) {
         if (o >= rmin && o <= omax) {
-            const unsigned long long v = wave_sum(tb[o]);
-            if (lane == 0) atomicAdd(&rb[16 + o], v);
+            const uint64_t v = wave_sum_u64(tb[o]);
+            if (lane == 0) atomicAdd(&rb[16 + o], (unsigned long long)v);
         }
     }
     __syncthreads();
@@ -404,27 +617,27 @@ __global__ __launch_bounds__(LMAX >= 16 ? 512 : 1024) void k_resid(ResidArgs a) 
     for (int K = tid; K < (1 << best); K += NT) rp[K] = hp[(1 << best) + K];
 }
 
-template <int LMAX, bool WIDE, typename ResT>
+template <int LMAX, int PATH, typename ResT>
 static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
-    const int nch = (a.n + 7) / 8;
-    int nt = 64 * ((nch + 64 * kCPT - 1) / (64 * kCPT));
-    if (nt < 64) nt = 64;
-    const size_t lds = resid_lds_bytes(LMAX, a.n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff), (int)sizeof(ResT));
-    auto kern = k_resid<LMAX, WIDE, ResT>;
+    const int nt = resid_threads(a.n);
+    const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff),
+                                        PATH == PATH_S16 ? 2 : 4, (int)sizeof(ResT), CoefTables<LMAX>::BYTES).total;
+    auto kern = k_resid<LMAX, PATH, ResT>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)a.count), dim3(nt), lds, s, a);
     return hipGetLastError();
 }
 
-
 template <int LMAX>
-static hipError_t launch_resid_bucket(const ResidArgs& a, bool wide, int rb, hipStream_t s) {
-    if (rb == 8) return launch_resid_T<LMAX, true, uint64_t>(a, s);
-    return wide ? launch_resid_T<LMAX, true, uint32_t>(a, s) : launch_resid_T<LMAX, false, uint32_t>(a, s);
+static hipError_t launch_resid_bucket(const ResidArgs& a, int path, int rb, hipStream_t s) {
+    if (rb == 8) return launch_resid_T<LMAX, PATH_W64, uint64_t>(a, s);
+    if (path == PATH_S16) return launch_resid_T<LMAX, PATH_S16, uint32_t>(a, s);
+    if (path == PATH_N32) return launch_resid_T<LMAX, PATH_N32, uint32_t>(a, s);
+    return launch_resid_T<LMAX, PATH_W64, uint32_t>(a, s);
 }
 
 }  // namespace flacmi

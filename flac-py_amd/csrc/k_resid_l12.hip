@@ -2,7 +2,7 @@
 #include "k_resid.h"
 
 namespace flacmi {
-hipError_t launch_resid_l12(const ResidArgs& a, bool wide, int rb, hipStream_t s) {
-    return launch_resid_bucket<12>(a, wide, rb, s);
+hipError_t launch_resid_l12(const ResidArgs& a, int path, int rb, hipStream_t s) {
+    return launch_resid_bucket<12>(a, path, rb, s);
 }
 }  // namespace flacmi
