@@ -54,6 +54,8 @@ SITE_NAMES = {
 
 MODE_REFERENCE = 0
 MODE_FIXED_ONLY = 1
+MODE_LPC_ONLY = 2
+MODE_RICE_ONLY = 3
 KIND_FIXED = 0
 KIND_LPC = 1
 

@@ -252,8 +252,12 @@ static int validate(const flacmi_batch* b, const flacmi_params* p, const flacmi_
     if (p->qlp_precision < 5 || p->qlp_precision > 31) return fail(FLACMI_E_INVALID, "qlp_precision must be 5..31");
     if (p->rice_min < 0 || p->rice_max > FLACMI_MAX_RICE_ORDER)
         return fail(FLACMI_E_INVALID, "rice partition orders must be within 0..15");
-    if (p->mode != FLACMI_MODE_REFERENCE && p->mode != FLACMI_MODE_FIXED_ONLY) return fail(FLACMI_E_INVALID, "bad mode");
-    if (p->mode == FLACMI_MODE_REFERENCE && b->sample_bits + p->qlp_precision > 44)
+    if (p->mode < FLACMI_MODE_REFERENCE || p->mode > FLACMI_MODE_RICE_ONLY) return fail(FLACMI_E_INVALID, "bad mode");
+    if (p->mode == FLACMI_MODE_RICE_ONLY && (p->reserved[0] < 0 || p->reserved[0] > FLACMI_MAX_LPC_ORDER))
+        return fail(FLACMI_E_INVALID, "RICE_ONLY predictor order (reserved[0]) must be 0..32");
+    if (p->mode == FLACMI_MODE_LPC_ONLY && p->max_lpc_order < 1)
+        return fail(FLACMI_E_INVALID, "LPC_ONLY needs max_lpc_order >= 1");
+    if (p->mode != FLACMI_MODE_FIXED_ONLY && p->mode != FLACMI_MODE_RICE_ONLY && b->sample_bits + p->qlp_precision > 44)
         return fail(FLACMI_E_UNSUPPORTED,
                     "sample_bits + qlp_precision > 44: candidate residual sums may exceed int64 (see DESIGN.md)");
     if (o->residual_bytes != 4 && o->residual_bytes != 8) return fail(FLACMI_E_INVALID, "residual_bytes must be 4 or 8");
@@ -280,7 +284,7 @@ static int validate(const flacmi_batch* b, const flacmi_params* p, const flacmi_
 static bool needs_wide(int n, int bits, int L, int q, int mode) {
     if (bits > 24 || q > 24) return true;
     const double xmax = ldexp(1.0, bits - 1);
-    const double rmax = mode == FLACMI_MODE_FIXED_ONLY ? 16.0 * xmax : xmax * (1.0 + (double)L * ldexp(1.0, q - 1)) + 16.0 * xmax;
+    const double rmax = (mode == FLACMI_MODE_FIXED_ONLY || mode == FLACMI_MODE_RICE_ONLY) ? 16.0 * xmax : xmax * (1.0 + (double)L * ldexp(1.0, q - 1)) + 16.0 * xmax;
     return rmax >= ldexp(1.0, 26) || rmax * resid_samples_per_thread(n) >= ldexp(1.0, 32);
 }
 
@@ -297,9 +301,10 @@ static int debug_stop() {
 static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi_params* p,
                                const flacmi_outputs* o, hipStream_t s) {
     if (int rc = set_device(ctx)) return rc;
-    const int L = p->mode == FLACMI_MODE_FIXED_ONLY ? 0 : p->max_lpc_order;
+    const bool lpc = p->mode == FLACMI_MODE_REFERENCE || p->mode == FLACMI_MODE_LPC_ONLY;
+    const int L = lpc ? p->max_lpc_order : 0;
     const int rec_words = FLACMI_LPC_REC_WORDS(L);
-    if (p->mode == FLACMI_MODE_REFERENCE) {
+    if (lpc) {
         if (int rc = ensure_buf(ctx->rec, sizeof(int32_t) * (size_t)rec_words * (size_t)(b->n_units > 0 ? b->n_units : 1)))
             return rc;
     }
@@ -315,12 +320,12 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         if (nfull > 0) cls[ncls++] = {0, nfull, b->block_len};
         cls[ncls++] = {nfull, b->n_tail_units, b->tail_len};
     }
-    if (o->acf && p->mode != FLACMI_MODE_REFERENCE)
+    if (o->acf && !lpc)
         HIP_TRY(hipMemsetAsync(o->acf, 0, sizeof(double) * 33 * b->n_units, s));
     hipEvent_t* ev = ctx->ev[ctx->ncalls % flacmi_ctx::kRing];
     HIP_TRY(hipEventRecord(ev[0], s));
     /* LPC analysis for every class first, then the residual pass */
-    for (int c = 0; c < ncls && p->mode == FLACMI_MODE_REFERENCE; ++c) {
+    for (int c = 0; c < ncls && lpc; ++c) {
         LpcArgs a{};
         a.samples = b->samples;
         a.stride = b->unit_stride;
@@ -350,7 +355,8 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.mode = p->mode;
         a.rmin = p->rice_min;
         a.rmax = p->rice_max;
-        a.rec = p->mode == FLACMI_MODE_REFERENCE ? (const int32_t*)ctx->rec.p + cls[c].unit0 * rec_words : nullptr;
+        a.rec = lpc ? (const int32_t*)ctx->rec.p + cls[c].unit0 * rec_words : nullptr;
+        a.rice_order = p->mode == FLACMI_MODE_RICE_ONLY ? p->reserved[0] : 0;
         a.rec_words = rec_words;
         a.log2thr = ctx->d_log2thr;
         a.meta = o->meta + cls[c].unit0;
@@ -368,7 +374,7 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
     HIP_TRY(hipEventRecord(ev[2], s));
     ctx->ncalls++;
     if (o->lpc_records) {
-        if (p->mode == FLACMI_MODE_REFERENCE) {
+        if (lpc) {
             HIP_TRY(launch_expand_records((const int32_t*)ctx->rec.p, rec_words, L, b->n_units, o->lpc_records, s));
         } else {
             HIP_TRY(hipMemsetAsync(o->lpc_records, 0, sizeof(int32_t) * FLACMI_LPC_REC_WORDS(32) * b->n_units, s));

@@ -31,6 +31,7 @@ struct ResidArgs {
     int32_t sample_bytes;
     int32_t n, L, mode;
     int32_t rmin, rmax;      /* rice range; rmax < rmin => empty */
+    int32_t rice_order;      /* predictor order in FLACMI_MODE_RICE_ONLY */
     const int32_t* rec;      /* [count][rec_words] (NULL in fixed-only mode) */
     int32_t rec_words;
     const double* log2thr;

@@ -117,7 +117,7 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes) {
 
 hipError_t launch_resid(const ResidArgs& a, int path, int residual_bytes, hipStream_t s) {
     if (a.count <= 0) return hipSuccess;
-    const int lb = a.mode == FLACMI_MODE_FIXED_ONLY ? 0 : lmax_bucket(a.L);
+    const int lb = (a.mode == FLACMI_MODE_FIXED_ONLY || a.mode == FLACMI_MODE_RICE_ONLY) ? 0 : lmax_bucket(a.L);
     switch (lb) {
         case 0: return launch_resid_l0(a, path, residual_bytes, s);
         case 8: return launch_resid_l8(a, path, residual_bytes, s);

@@ -228,8 +228,10 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     const int n = a.n, L = a.L;
     const int nch = (n + 7) >> 3;
     const int npad = nch * 8 + 8;
-    const bool ref_mode = a.mode == FLACMI_MODE_REFERENCE;
+    /* LPC records exist in the reference and LPC-only modes */
+    const bool ref_mode = a.mode == FLACMI_MODE_REFERENCE || a.mode == FLACMI_MODE_LPC_ONLY;
     const bool do_lpc = LMAX > 0 && ref_mode;
+    const bool rice_only = a.mode == FLACMI_MODE_RICE_ONLY;
 
     /* ---- LDS carve (integer offsets keep every access a ds_* instruction) ---- */
     int rmax_eff = -1;
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
 #pragma unroll
     for (int s = 0; s < NSUM; ++s) acc[s] = 0;
 #pragma unroll 1
-    for (int c = tid; c < nch; c += NT) {
+    for (int c = rice_only ? nch : tid; c < nch; c += NT) {
         const int i0 = 8 * c;
         const bool fast = (i0 >= HP) && (i0 + 8 <= n);
         if constexpr (S16) {
@@ -379,13 +381,26 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         d.lpc_order = 0;
         d.lpc_sum = 0;
         for (int j = 0; j < FLACMI_MAX_LPC_ORDER; ++j) d.coef[j] = j < 4 ? c_fixed_coef[fo][j] : 0;
+        if (rice_only) {
+            d.fixed_order = 0;
+            d.fixed_sum = 0;
+            d.order = a.rice_order; /* identity "predictor": the row already is the residual */
+            for (int j = 0; j < 4; ++j) d.coef[j] = 0;
+        }
         if (do_lpc) {
             int best = 1;
             for (int pp = 2; pp <= L; ++pp)
                 if (tot[4 + pp] < tot[4 + best]) best = pp;
             d.lpc_order = best;
             d.lpc_sum = (long long)tot[4 + best];
-            if (tot[4 + best] < tot[fo]) {
+            if (a.mode == FLACMI_MODE_LPC_ONLY) {
+                d.kind = FLACMI_KIND_LPC;
+                d.order = best;
+                d.shift = lsh[best - 1];
+                d.ncoefs = lsh[LMAX + best - 1] == 0 ? 0 : best;
+                for (int j = 0; j < FLACMI_MAX_LPC_ORDER; ++j)
+                    d.coef[j] = j < best ? cfl[(best - 1) * CT::CPAD + j] : 0;
+            } else if (tot[4 + best] < tot[fo]) {
                 /* A coefficient-less candidate (negative-shift branch) sums |x| over all n
                  * samples, exactly the fixed order-0 sum, so it never gets here. */
                 d.kind = FLACMI_KIND_LPC;
@@ -415,7 +430,9 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     if (a.stop_after == 3) return;
     const int order = dec->order;
     const int dshift = dec->shift;
-    const int start = order; /* the residual starts at index len(warmup) */
+    /* the residual starts at index len(warmup); a coefficient-less LPC subframe (only
+     * reachable in LPC-only mode) keeps every sample */
+    const int start = (dec->kind == FLACMI_KIND_LPC && dec->ncoefs == 0) ? 0 : order;
     constexpr int TAPS = LMAX > 4 ? LMAX : 4;
 
     /* ---- phase E: chosen residual, zig-zag, to LDS and HBM ---- */
@@ -507,6 +524,15 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     if (a.stop_after == 4) return;
     if (misc[2]) {
         if (tid == 0) put_meta(meta, FLACMI_STATUS_RESIDUAL_WIDE, FLACMI_SITE_RESIDUAL_WIDTH, dec, 1);
+        return;
+    }
+    if (a.mode == FLACMI_MODE_LPC_ONLY) {
+        if (tid == 0) {
+            put_meta(meta, ST_OK, 0, dec, 1);
+            meta->res_offset = start;
+            meta->res_len = n - start;
+            meta->part_order = -1;
+        }
         return;
     }
 

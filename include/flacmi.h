@@ -88,6 +88,12 @@ enum flacmi_mode {
     FLACMI_MODE_REFERENCE = 0,   /* fixed + LPC + choice + Rice, exactly as encode() does */
     FLACMI_MODE_FIXED_ONLY = 1,  /* fixed predictor + Rice only (BASELINE config 5; the
                                     reference's own -l 0 raises ValueError instead) */
+    FLACMI_MODE_LPC_ONLY = 2,    /* encode_subframe_lpc alone (encoder.py:362-420): the best LPC
+                                    candidate is the result, no fixed comparison, no Rice search
+                                    (part_order = -1); its residual row is returned */
+    FLACMI_MODE_RICE_ONLY = 3,   /* encode_residual alone (encoder.py:632-652): each row holds a
+                                    residual at [reserved[0], len) for predictor order
+                                    params.reserved[0]; only the Rice search runs */
 };
 
 enum flacmi_kind { FLACMI_KIND_FIXED = 0, FLACMI_KIND_LPC = 1 };
@@ -98,7 +104,7 @@ typedef struct flacmi_params {
     int32_t rice_min;        /* rice_partition_order.start */
     int32_t rice_max;        /* rice_partition_order.stop - 1 (rice_max < rice_min: empty range) */
     int32_t mode;            /* flacmi_mode */
-    int32_t reserved[3];
+    int32_t reserved[3];     /* reserved[0]: predictor order in FLACMI_MODE_RICE_ONLY, else 0 */
 } flacmi_params;
 
 /* One batch of units.  Samples are planar: unit u occupies

@@ -235,6 +235,20 @@ int oracle_analyze_unit(const int64_t* x, int32_t n, const flacmi_params* p,
     int64_t* lres = tmp + (size_t)5 * (n + 1);
     int rc = 0;
 
+    if (p->mode == FLACMI_MODE_RICE_ONLY) { /* encode_residual alone (encoder.py:632-652) */
+        const int order = p->reserved[0];
+        const int len = n - order > 0 ? n - order : 0;
+        for (int i = 0; i < len; i++) lres[i] = x[order + i];
+        meta->order = order;
+        meta->res_offset = order;
+        meta->res_len = len;
+        uint64_t* zz = residual ? residual + order : (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(n + 1));
+        rc = encode_residual(lres, len, n, order, p, meta, rice_params, zz);
+        if (!residual) free(zz);
+        free(tmp);
+        return rc;
+    }
+
     /* ---- encode_subframe_fixed (encoder.py:331-359) ---- */
     int64_t fsum[5] = {0, 0, 0, 0, 0};
     int forder = 0;
@@ -259,7 +273,7 @@ int oracle_analyze_unit(const int64_t* x, int32_t n, const flacmi_params* p,
     int32_t chosen_len = n - (n <= 4 ? 0 : forder);
     if (n <= 4) res_offset = 0;
 
-    if (p->mode == FLACMI_MODE_REFERENCE) {
+    if (p->mode == FLACMI_MODE_REFERENCE || p->mode == FLACMI_MODE_LPC_ONLY) {
         /* ---- encode_subframe_lpc (encoder.py:362-420) ---- */
         double* w = (double*)malloc(sizeof(double) * (size_t)n * 2);
         double* win = w + n;
@@ -320,7 +334,30 @@ int oracle_analyze_unit(const int64_t* x, int32_t n, const flacmi_params* p,
         }
         meta->lpc_order = best;
         meta->lpc_sum = best_sum;
-        /* ---- choice, encoder.py:135-157 ---- */
+        /* ---- choice, encoder.py:135-157 (LPC-only mode: encode_subframe_lpc alone) ---- */
+        if (p->mode == FLACMI_MODE_LPC_ONLY) {
+            meta->kind = FLACMI_KIND_LPC;
+            meta->order = best;
+            meta->shift = qs[best - 1];
+            meta->ncoefs = nq[best - 1];
+            for (int j = 0; j < nq[best - 1]; j++) meta->coefs[j] = qc[best - 1][j];
+            int32_t len;
+            if (nq[best - 1] == 0) {
+                for (int i = 0; i < n; i++) lres[i] = x[i];
+                len = n;
+                meta->res_offset = 0;
+            } else {
+                prediction_residual(x, n, qc[best - 1], nq[best - 1], qs[best - 1], lres);
+                len = n - nq[best - 1];
+                meta->res_offset = best;
+            }
+            meta->res_len = len;
+            meta->part_order = -1;
+            if (residual)
+                for (int i = 0; i < len; i++)
+                    residual[meta->res_offset + i] = ((uint64_t)lres[i] << 1) ^ (uint64_t)(lres[i] >> 63);
+            goto done;
+        }
         if (fsum[forder] < best_sum) {
             /* fixed wins: already set */
         } else if (best_sum < fsum[forder]) {
