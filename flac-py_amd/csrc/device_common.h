@@ -165,8 +165,11 @@ __host__ __device__ constexpr int resid_hp(int lmax) { return lmax > 4 ? ((lmax 
 /* LDS layout of k_resid: byte offsets (multiples of 16) from the dynamic LDS base.  The
  * host sizes the allocation with the same function the kernel carves it with. */
 struct ResidLds {
-    int xs, zz, coef, red, tot, dec, rb, misc, hs, hp, total;
+    int xs, zz, coef, red, tot, dec, rb, misc, hs, hp, tl, total;
 };
+/* floor(log2) thresholds staged in LDS for exponents [kTlLo, kTlLo + 64): every Rice
+ * mean S/len of a 32-bit residual (S >= 1, len <= 65535, S < 2^48) falls inside. */
+constexpr int kTlLo = -16;
 __host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, int P, int xbytes, int zbytes,
                                                      int coef_bytes) {
     auto up = [](int b) { return (b + 15) & ~15; };
@@ -177,13 +180,14 @@ __host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, in
     l.xs = o;   o = up(o + xbytes * (resid_hp(lmax) + npad));
     l.zz = o;   o = up(o + zbytes * npad);
     l.coef = o; o = up(o + coef_bytes);
-    l.red = o;  o = up(o + 8 * nw * nsum);
+    l.red = o;  o = up(o + 8 * nw * (nsum > 16 ? nsum : 16));
     l.tot = o;  o = up(o + 8 * nsum);
     l.dec = o;  o = up(o + (int)sizeof(Decision));
     l.rb = o;   o = up(o + 8 * 32);
-    l.misc = o; o = up(o + 4 * 4);
+    l.misc = o; o = up(o + 4 * 8);
     l.hs = o;   o = up(o + 8 * 2 * P);
     l.hp = o;   o = up(o + 4 * 2 * P);
+    l.tl = o;   o = up(o + 8 * 64);
     l.total = o;
     return l;
 }

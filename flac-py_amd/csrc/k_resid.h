@@ -107,9 +107,15 @@ struct CoefTables {
     static constexpr int NP = (LMAX + 1) / 2;                       /* pairs per order */
     static constexpr int PPAD = NP > 0 ? ((NP + 3) / 4) * 4 : 4;    /* padded to uint4 */
     static constexpr int CPAD = LMAX > 0 ? ((LMAX + 3) / 4) * 4 : 4;
-    static constexpr int BYTES = 16 * ((4 * LMAX * (PPAD + CPAD) + 8 * LMAX + 15) / 16);
+    static constexpr int BYTES = 16 * ((4 * LMAX * (PPAD + CPAD) + 16 * LMAX + 15) / 16);
 };
 
+/* PATH_S16 candidate sums.  With t = 2^31 - x[i]*2^sh + pred (exact: |x| <= 2^15,
+ * sh <= 15 and |pred| < 2^26, so t is in [0, 2^32)), the logical shift t >> sh equals
+ * 2^(31-sh) + (pred >> sh) - x[i], so |r| = |(t >> sh) - 2^(31-sh)| is one v_sad_u32:
+ * per sample and order one v_mad_i32_i24 (the dot chain's initial value), ceil(p/2)
+ * v_dot2_i32_i16, one shift and one v_sad_u32 accumulate.  The eight samples of a chunk
+ * run as independent chains, interleaved tap by tap. */
 template <int LMAX, int HP, bool MASKED>
 __device__ __forceinline__ void chunk_sums_s16(const Win16<HP>& W, int i0, int n, int L, bool do_lpc,
                                                const uint32_t* cpair, const int32_t* lsh,
@@ -134,17 +140,25 @@ __device__ __forceinline__ void chunk_sums_s16(const Win16<HP>& W, int i0, int n
             }
             const int sh = lsh[pp - 1];
             const int start = lsh[LMAX + pp - 1];
+            const int32_t negp = lsh[2 * LMAX + pp - 1];           /* -(2^sh) */
+            const uint32_t kb = (uint32_t)lsh[3 * LMAX + pp - 1];  /* 2^(31-sh) */
+            int32_t t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] = (int32_t)((uint32_t)(sext24(W.x[4 + k]) * sext24(negp)) + kBias);
+#pragma unroll
+            for (int j = 0; j < np; ++j)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t[k] = sdot2(W.pair(k, j), cq[j], t[k]);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                int32_t pred = 0;
-#pragma unroll
-                for (int t = 0; t < np; ++t) pred = sdot2(W.pair(k, t), cq[t], pred);
-                uint32_t s = sad_acc((uint32_t)W.x[4 + k] ^ kBias, (uint32_t)(pred >> sh) ^ kBias, 0);
+                const uint32_t u = (uint32_t)t[k] >> sh;
                 if (MASKED) {
                     const int i = i0 + k;
-                    s = (i >= start && i < n) ? s : 0;
+                    const uint32_t s = sad_acc(u, kb, 0);
+                    acc[4 + pp] += (i >= start && i < n) ? s : 0u;
+                } else {
+                    acc[4 + pp] = sad_acc(u, kb, acc[4 + pp]);
                 }
-                acc[4 + pp] += s;
             }
         }
     });
@@ -211,6 +225,132 @@ __device__ __forceinline__ void chunk_sums_32(const int32_t (&w)[HP + 8], int i0
     });
 }
 
+/* floor(log2(x)) for a Rice mean x (normal, > 0): LDS thresholds, global table outside. */
+__device__ __forceinline__ int rice_floor_log2(double x, const double* tl, const double* gthr) {
+    const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
+    if (e >= kTlLo && e < kTlLo + 64) return x >= tl[e - kTlLo] ? e + 1 : e;
+    return pym::py_floor_log2(x, gthr);
+}
+
+/* Rice partition search (encoder.py:655-760) for a 32-bit residual whose finest partitions
+ * are whole 8-sample chunks and number at most 64.
+ *  1. wave 0, lane k = finest partition k: its sum S_k from the zig-zag row in LDS;
+ *     a butterfly (shfl_xor) then gives every lane the sum of its ancestor at each order,
+ *     lane k computes that node's parameter floor(log2(S/len)) and writes it to
+ *     pk[k][order]; group leaders contribute the partition headers; the first error in the
+ *     reference's evaluation order (orders, then partitions, ascending) is kept.
+ *  2. every thread, per chunk it owns: sum over the chunk of x >> p for each candidate
+ *     order (parameters from pk of the chunk's finest partition), u64 per thread.
+ *  3. one workgroup reduction per order; thread 0 picks the order (first minimum). */
+template <typename ResT>
+__device__ __forceinline__ void rice_search_fast(const ResidArgs& a, flacmi_unit_meta* meta, const Decision* dec,
+                                              const ResT* zz, const double* tl, unsigned long long* rb,
+                                              unsigned long long* red, int* misc, uint8_t* pk, int n, int order,
+                                              int start, int rmin, int omax, int nch, int tid, int NT, int lane,
+                                              int wid, int nw, int64_t gid) {
+    const int P = 1 << omax, ps = n >> omax, cpp = ps >> 3;
+    if (wid == 0) {
+        const int k = lane;
+        uint64_t s = 0;
+        if (k < P) {
+            const uint4* z4 = reinterpret_cast<const uint4*>(zz + k * ps);
+            for (int c = 0; c < cpp; ++c) {
+                const uint4 u = z4[2 * c], v = z4[2 * c + 1];
+                s += (uint64_t)(u.x + u.y + u.z + u.w + v.x + v.y + v.z + v.w);
+            }
+        }
+        int ekey = -1, esite = 0;
+        uint32_t m5 = 0;
+        for (int o = omax; o >= rmin; --o) {
+            const int d = omax - o;
+            if (d > 0) s += (uint64_t)__shfl_xor((unsigned long long)s, 1 << (d - 1));
+            const int K = k >> d;
+            const bool lead = k < P && (k & ((1 << d) - 1)) == 0;
+            const int len = (n >> o) - (K == 0 ? order : 0);
+            int prm = 0;
+            bool zero = s == 0, neg = false;
+            if (!zero) {
+                prm = rice_floor_log2((double)s / (double)len, tl, a.log2thr);
+                neg = prm < 0;
+            }
+            if (k < P) pk[16 * k + o] = (uint8_t)prm;
+            const unsigned long long eb = __ballot(lead && (zero || neg));
+            if (eb) {
+                const int kl = __builtin_ctzll(eb);
+                ekey = (o << 16) | (kl >> d);
+                esite = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
+            }
+            if (__ballot(lead && prm > 14)) m5 |= 1u << o;
+            uint64_t hb = lead ? 4ull + (prm > 14 ? 5ull : 4ull) + (uint64_t)len * (uint64_t)(1 + prm) : 0ull;
+            hb = wave_sum_u64(hb);
+            if (lane == 0) rb[o] = hb;
+        }
+        if (lane == 0) {
+            misc[0] = ekey;
+            misc[1] = esite;
+            misc[4] = (int)m5;
+        }
+    }
+    __syncthreads();
+    if (misc[0] >= 0) {
+        if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
+        return;
+    }
+    /* data bits per candidate order */
+    const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+    uint64_t tb[16];
+#pragma unroll
+    for (int o = 0; o < 16; ++o) tb[o] = 0;
+    for (int c = tid; c < nch; c += NT) {
+        const int k = c / cpp;
+        if (k >= P) break; /* the zero pad chunk past n */
+        const uint4 pv = *reinterpret_cast<const uint4*>(pk + 16 * k);
+        const uint4 u = reinterpret_cast<const uint4*>(zz)[2 * c], v = reinterpret_cast<const uint4*>(zz)[2 * c + 1];
+        const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+        for (int o = 0; o < 16; ++o) {
+            if (o >= ro && o <= oo) {
+                const uint32_t p = (pw[o >> 2] >> (8 * (o & 3))) & 0xffu;
+                const uint32_t t = (u.x >> p) + (u.y >> p) + (u.z >> p) + (u.w >> p) + (v.x >> p) + (v.y >> p) +
+                                   (v.z >> p) + (v.w >> p);
+                tb[o] += t;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < 16; ++o) {
+        if (o >= ro && o <= oo) {
+            const uint64_t w = wave_sum_u64(tb[o]);
+            if (lane == 0) red[wid * 16 + o] = w;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int best = -1;
+        unsigned long long bb = 0;
+        for (int o = rmin; o <= omax; ++o) {
+            unsigned long long v = rb[o];
+            for (int w2 = 0; w2 < nw; ++w2) v += red[w2 * 16 + o];
+            if (best < 0 || v < bb) {
+                bb = v;
+                best = o;
+            }
+        }
+        put_meta(meta, ST_OK, 0, dec, 1);
+        meta->res_offset = start;
+        meta->res_len = n - start;
+        meta->part_order = best;
+        meta->n_parts = 1 << best;
+        meta->coding_method = ((misc[4] >> best) & 1) ? 5 : 4;
+        meta->rice_bits = (long long)bb;
+        misc[3] = best;
+    }
+    __syncthreads();
+    const int best = misc[3];
+    int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
+    for (int K = tid; K < (1 << best); K += NT) rp[K] = pk[16 * (K << (omax - best)) + best];
+}
+
 template <int LMAX, int PATH, typename ResT>
 __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     using UX = ResT;
@@ -244,7 +384,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     ResT* zz = reinterpret_cast<ResT*>(smem + lay.zz);              /* [npad] */
     uint32_t* cpair = reinterpret_cast<uint32_t*>(smem + lay.coef);  /* [LMAX][PPAD] */
     int32_t* cfl = reinterpret_cast<int32_t*>(smem + lay.coef + 4 * LMAX * CT::PPAD); /* [LMAX][CPAD] */
-    int32_t* lsh = cfl + LMAX * CT::CPAD;                            /* [2*LMAX] shift, start */
+    int32_t* lsh = cfl + LMAX * CT::CPAD; /* [4*LMAX] shift, start, -(2^shift), 2^(31-shift) */
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + lay.red);
     unsigned long long* tot = reinterpret_cast<unsigned long long*>(smem + lay.tot);
     Decision* dec = reinterpret_cast<Decision*>(smem + lay.dec);
@@ -252,6 +392,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     int* misc = reinterpret_cast<int*>(smem + lay.misc);
     unsigned long long* hs = reinterpret_cast<unsigned long long*>(smem + lay.hs);
     int32_t* hp = reinterpret_cast<int32_t*>(smem + lay.hp);
+    double* tl = reinterpret_cast<double*>(smem + lay.tl); /* log2 thresholds, e in [kTlLo, kTlLo+64) */
     flacmi_unit_meta* meta = a.meta + gid;
     const int32_t* __restrict__ rec = ref_mode ? a.rec + gid * a.rec_words : nullptr;
 
@@ -305,8 +446,11 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
             cpair[i] = ((uint32_t)hi << 16) | ((uint32_t)lo & 0xffffu);
         }
         for (int i = tid; i < LMAX; i += NT) {
-            lsh[i] = i < L ? rec[2 + i] : 0;
+            const int sh = i < L ? rec[2 + i] : 0; /* 0..15 */
+            lsh[i] = sh;
             lsh[LMAX + i] = ((negmask >> i) & 1) ? 0 : i + 1; /* first residual index */
+            lsh[2 * LMAX + i] = -(1 << sh);
+            lsh[3 * LMAX + i] = (int32_t)(1u << (31 - sh));
         }
     }
     if (tid == 0) {
@@ -315,6 +459,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         misc[2] = 0;
     }
     if (tid < 32) rb[tid] = 0;
+    if (tid < 64) tl[tid] = a.log2thr[tid + kTlLo + 1074];
     __syncthreads();
     if (a.stop_after == 1) return;
 
@@ -546,6 +691,14 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     }
     const int rmin = a.rmin;
     const int P = 1 << omax, ps = n >> omax;
+    if constexpr (!WIDE) {
+        /* zz < 2^27 here, so a chunk of eight fits 32 bits */
+        if ((ps & 7) == 0 && P <= 64) {
+            rice_search_fast(a, meta, dec, zz, tl, rb, red, misc, reinterpret_cast<uint8_t*>(hs), n, order, start,
+                             rmin, omax, nch, tid, NT, lane, wid, nw, gid);
+            return;
+        }
+    }
     /* finest partition sums: heap nodes [P, 2P); zz[i] = 0 for i < start */
     for (int k = wid; k < P; k += nw) {
         const int lo = k * ps, hi = (k + 1) * ps;
