@@ -105,6 +105,17 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+/* u32 wave total (exact while the true total < 2^32); one v_add_u32_dpp per step */
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    v += dpp_u32<0xB1, 0xf>(v);
+    v += dpp_u32<0x4E, 0xf>(v);
+    v += dpp_u32<0x141, 0xf>(v);
+    v += dpp_u32<0x140, 0xf>(v);
+    v += dpp_u32<0x142, 0xa>(v);
+    v += dpp_u32<0x143, 0xc>(v);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 /* |a - b| + c on biased (x ^ 0x80000000) operands: one v_sad_u32. */
 __device__ __forceinline__ uint32_t sad_acc(uint32_t a, uint32_t b, uint32_t c) {
     return (a > b ? a - b : b - a) + c;
@@ -162,26 +173,34 @@ __host__ __device__ inline int resid_samples_per_thread(int n) {
 /* History pad in front of the staged samples (>= LMAX and >= 4, multiple of 8). */
 __host__ __device__ constexpr int resid_hp(int lmax) { return lmax > 4 ? ((lmax + 7) / 8) * 8 : 8; }
 
+/* k_resid keeps the chosen zig-zag residual in registers (kCPT chunks of 8 per thread)
+ * instead of LDS when it is 32-bit and narrow (< 2^27), every thread owns at most kCPT
+ * chunks, and every candidate Rice order has whole-chunk finest partitions, at most 64. */
+__host__ __device__ inline bool resid_regz(int n, int rmax_eff, bool narrow32) {
+    const int pe = rmax_eff < 0 ? 0 : rmax_eff;
+    return narrow32 && n <= 8 * kCPT * 256 && n % (8 << pe) == 0 && (1 << pe) <= 64;
+}
+
 /* LDS layout of k_resid: byte offsets (multiples of 16) from the dynamic LDS base.  The
  * host sizes the allocation with the same function the kernel carves it with. */
 struct ResidLds {
-    int xs, zz, coef, red, tot, dec, rb, misc, hs, hp, tl, total;
+    int xs, zz, cs, coef, red, dec, rb, misc, hs, hp, tl, total;
 };
 /* floor(log2) thresholds staged in LDS for exponents [kTlLo, kTlLo + 64): every Rice
  * mean S/len of a 32-bit residual (S >= 1, len <= 65535, S < 2^48) falls inside. */
 constexpr int kTlLo = -16;
 __host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, int P, int xbytes, int zbytes,
-                                                     int coef_bytes) {
+                                                     int coef_bytes, bool regz) {
     auto up = [](int b) { return (b + 15) & ~15; };
     const int nsum = 5 + lmax;
     const int npad = ((n + 7) / 8) * 8 + 8;
     ResidLds l;
     int o = 0;
     l.xs = o;   o = up(o + xbytes * (resid_hp(lmax) + npad));
-    l.zz = o;   o = up(o + zbytes * npad);
+    l.zz = o;   o = up(o + (regz ? 0 : zbytes * npad)); /* zig-zag row (LDS-resident mode) */
+    l.cs = o;   o = up(o + (regz ? 4 * (npad / 8) : 0)); /* chunk sums (register-resident mode) */
     l.coef = o; o = up(o + coef_bytes);
     l.red = o;  o = up(o + 8 * nw * (nsum > 16 ? nsum : 16));
-    l.tot = o;  o = up(o + 8 * nsum);
     l.dec = o;  o = up(o + (int)sizeof(Decision));
     l.rb = o;   o = up(o + 8 * 32);
     l.misc = o; o = up(o + 4 * 8);

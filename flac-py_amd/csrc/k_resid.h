@@ -54,9 +54,11 @@ struct Win16 {
             x[t] = (pos & 1) ? ((int32_t)pr >> 16) : (int32_t)(int16_t)(pr & 0xffff);
         }
     }
-    /* pair of taps (2t, 2t+1) for the sample at window position HP + k */
+    /* (x[i-1-2t] lo, x[i-2t] hi) for the sample i at window position HP + k.  Position -1
+     * only occurs as the lo half of the last pair of an even LMAX = HP, whose coefficient is 0. */
     __device__ __forceinline__ uint32_t pair(int k, int t) const {
-        const int lo = HP + k - 2 - 2 * t; /* index of x[i-2-2t] */
+        const int lo = HP + k - 1 - 2 * t;
+        if (lo < 0) return E[0] << 16;
         return (lo & 1) ? O[(lo - 1) >> 1] : E[lo >> 1];
     }
 };
@@ -104,18 +106,18 @@ __device__ __forceinline__ void fixed_sums32(const int32_t (&x)[12], int i0, int
 /* LDS tables of the LPC candidates, filled in phase A */
 template <int LMAX>
 struct CoefTables {
-    static constexpr int NP = (LMAX + 1) / 2;                       /* pairs per order */
+    static constexpr int NP = (LMAX + 2) / 2; /* pairs per order: taps x[i], x[i-1] .. x[i-LMAX] */
     static constexpr int PPAD = NP > 0 ? ((NP + 3) / 4) * 4 : 4;    /* padded to uint4 */
     static constexpr int CPAD = LMAX > 0 ? ((LMAX + 3) / 4) * 4 : 4;
-    static constexpr int BYTES = 16 * ((4 * LMAX * (PPAD + CPAD) + 16 * LMAX + 15) / 16);
+    static constexpr int BYTES = 16 * ((4 * LMAX * (PPAD + CPAD) + 12 * LMAX + 15) / 16);
 };
 
-/* PATH_S16 candidate sums.  With t = 2^31 - x[i]*2^sh + pred (exact: |x| <= 2^15,
- * sh <= 15 and |pred| < 2^26, so t is in [0, 2^32)), the logical shift t >> sh equals
- * 2^(31-sh) + (pred >> sh) - x[i], so |r| = |(t >> sh) - 2^(31-sh)| is one v_sad_u32:
- * per sample and order one v_mad_i32_i24 (the dot chain's initial value), ceil(p/2)
- * v_dot2_i32_i16, one shift and one v_sad_u32 accumulate.  The eight samples of a chunk
- * run as independent chains, interleaved tap by tap. */
+/* PATH_S16 candidate sums.  The dot chain of order p carries one extra tap, x[i] with
+ * coefficient -2^sh, and starts from 2^31: t = 2^31 + pred - x[i]*2^sh.  That is exact in
+ * [0, 2^32) (|x| <= 2^15, sh <= 15, |pred| < 2^26), so the logical shift t >> sh equals
+ * 2^(31-sh) + (pred >> sh) - x[i] and |r| = |(t >> sh) - 2^(31-sh)| is one v_sad_u32
+ * accumulate.  Per sample and order: ceil((p+1)/2) v_dot2_i32_i16, a shift and a sad.
+ * The eight samples of a chunk run as independent chains, interleaved tap by tap. */
 template <int LMAX, int HP, bool MASKED>
 __device__ __forceinline__ void chunk_sums_s16(const Win16<HP>& W, int i0, int n, int L, bool do_lpc,
                                                const uint32_t* cpair, const int32_t* lsh,
@@ -125,7 +127,7 @@ __device__ __forceinline__ void chunk_sums_s16(const Win16<HP>& W, int i0, int n
     if (!do_lpc) return;
     static_for<LMAX>([&](auto P_) {
         constexpr int pp = P_ + 1;
-        constexpr int np = (pp + 1) / 2;
+        constexpr int np = (pp + 2) / 2;
         __builtin_amdgcn_sched_barrier(0); /* one candidate at a time: bounds register pressure */
         if (pp <= L) {
             uint32_t cq[np];
@@ -140,13 +142,12 @@ __device__ __forceinline__ void chunk_sums_s16(const Win16<HP>& W, int i0, int n
             }
             const int sh = lsh[pp - 1];
             const int start = lsh[LMAX + pp - 1];
-            const int32_t negp = lsh[2 * LMAX + pp - 1];           /* -(2^sh) */
-            const uint32_t kb = (uint32_t)lsh[3 * LMAX + pp - 1];  /* 2^(31-sh) */
+            const uint32_t kb = (uint32_t)lsh[2 * LMAX + pp - 1]; /* 2^(31-sh) */
             int32_t t[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) t[k] = (int32_t)((uint32_t)(sext24(W.x[4 + k]) * sext24(negp)) + kBias);
+            for (int k = 0; k < 8; ++k) t[k] = sdot2(W.pair(k, 0), cq[0], (int32_t)kBias);
 #pragma unroll
-            for (int j = 0; j < np; ++j)
+            for (int j = 1; j < np; ++j)
 #pragma unroll
                 for (int k = 0; k < 8; ++k) t[k] = sdot2(W.pair(k, j), cq[j], t[k]);
 #pragma unroll
@@ -232,97 +233,93 @@ __device__ __forceinline__ int rice_floor_log2(double x, const double* tl, const
     return pym::py_floor_log2(x, gthr);
 }
 
-/* Rice partition search (encoder.py:655-760) for a 32-bit residual whose finest partitions
- * are whole 8-sample chunks and number at most 64.
- *  1. wave 0, lane k = finest partition k: its sum S_k from the zig-zag row in LDS;
- *     a butterfly (shfl_xor) then gives every lane the sum of its ancestor at each order,
- *     lane k computes that node's parameter floor(log2(S/len)) and writes it to
- *     pk[k][order]; group leaders contribute the partition headers; the first error in the
- *     reference's evaluation order (orders, then partitions, ascending) is kept.
+/* Rice partition search (encoder.py:655-760) when the residual is 32-bit and narrow, the
+ * finest partitions are whole 8-sample chunks and number at most 64:
+ *  1. wave 0, lane k = finest partition k, holding its sum S_k: a butterfly (shfl_xor)
+ *     gives every lane the sum of its ancestor at each order; the lane computes that
+ *     node's parameter floor(log2(S/len)) into pk[k][order]; group leaders add the
+ *     partition headers; the first error in the reference's evaluation order (orders, then
+ *     partitions, ascending) is kept (rice_params_wave0);
  *  2. every thread, per chunk it owns: sum over the chunk of x >> p for each candidate
- *     order (parameters from pk of the chunk's finest partition), u64 per thread.
- *  3. one workgroup reduction per order; thread 0 picks the order (first minimum). */
-template <typename ResT>
-__device__ __forceinline__ void rice_search_fast(const ResidArgs& a, flacmi_unit_meta* meta, const Decision* dec,
-                                              const ResT* zz, const double* tl, unsigned long long* rb,
-                                              unsigned long long* red, int* misc, uint8_t* pk, int n, int order,
-                                              int start, int rmin, int omax, int nch, int tid, int NT, int lane,
-                                              int wid, int nw, int64_t gid) {
-    const int P = 1 << omax, ps = n >> omax, cpp = ps >> 3;
-    if (wid == 0) {
-        const int k = lane;
-        uint64_t s = 0;
-        if (k < P) {
-            const uint4* z4 = reinterpret_cast<const uint4*>(zz + k * ps);
-            for (int c = 0; c < cpp; ++c) {
-                const uint4 u = z4[2 * c], v = z4[2 * c + 1];
-                s += (uint64_t)(u.x + u.y + u.z + u.w + v.x + v.y + v.z + v.w);
-            }
+ *     order, parameters from pk of the chunk's finest partition (chunk_rice_bits);
+ *  3. one wave reduction per order; thread 0 picks the order, first minimum (rice_finish). */
+__device__ __forceinline__ void rice_params_wave0(const ResidArgs& a, uint64_t s, const double* tl,
+                                                  unsigned long long* rb, int* misc, uint8_t* pk, int n, int order,
+                                                  int rmin, int omax, int lane) {
+    const int P = 1 << omax, k = lane;
+    int ekey = -1, esite = 0;
+    uint32_t m5 = 0;
+    for (int o = omax; o >= rmin; --o) {
+        const int d = omax - o;
+        if (d > 0) s += (uint64_t)__shfl_xor((unsigned long long)s, 1 << (d - 1));
+        const int K = k >> d;
+        const bool lead = k < P && (k & ((1 << d) - 1)) == 0;
+        const int len = (n >> o) - (K == 0 ? order : 0);
+        int prm = 0;
+        const bool zero = s == 0;
+        bool neg = false;
+        if (!zero) {
+            prm = rice_floor_log2((double)s / (double)len, tl, a.log2thr);
+            neg = prm < 0;
         }
-        int ekey = -1, esite = 0;
-        uint32_t m5 = 0;
-        for (int o = omax; o >= rmin; --o) {
-            const int d = omax - o;
-            if (d > 0) s += (uint64_t)__shfl_xor((unsigned long long)s, 1 << (d - 1));
-            const int K = k >> d;
-            const bool lead = k < P && (k & ((1 << d) - 1)) == 0;
-            const int len = (n >> o) - (K == 0 ? order : 0);
-            int prm = 0;
-            bool zero = s == 0, neg = false;
-            if (!zero) {
-                prm = rice_floor_log2((double)s / (double)len, tl, a.log2thr);
-                neg = prm < 0;
-            }
-            if (k < P) pk[16 * k + o] = (uint8_t)prm;
-            const unsigned long long eb = __ballot(lead && (zero || neg));
-            if (eb) {
-                const int kl = __builtin_ctzll(eb);
-                ekey = (o << 16) | (kl >> d);
-                esite = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
-            }
-            if (__ballot(lead && prm > 14)) m5 |= 1u << o;
-            uint64_t hb = lead ? 4ull + (prm > 14 ? 5ull : 4ull) + (uint64_t)len * (uint64_t)(1 + prm) : 0ull;
-            hb = wave_sum_u64(hb);
-            if (lane == 0) rb[o] = hb;
+        if (k < P) pk[16 * k + o] = (uint8_t)prm;
+        const unsigned long long eb = __ballot(lead && (zero || neg));
+        if (eb) {
+            const int kl = __builtin_ctzll(eb);
+            ekey = (o << 16) | (kl >> d);
+            esite = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
         }
-        if (lane == 0) {
-            misc[0] = ekey;
-            misc[1] = esite;
-            misc[4] = (int)m5;
-        }
+        if (__ballot(lead && prm > 14)) m5 |= 1u << o;
+        /* headers: < 2^23 per partition, so the order's total fits 32 bits */
+        const uint32_t hb = lead ? 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm) : 0u;
+        const uint32_t ht = wave_sum_u32(hb);
+        if (lane == 0) rb[o] = ht;
     }
-    __syncthreads();
-    if (misc[0] >= 0) {
-        if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
-        return;
+    if (lane == 0) {
+        misc[0] = ekey;
+        misc[1] = esite;
+        misc[4] = (int)m5;
     }
-    /* data bits per candidate order */
-    const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
-    uint64_t tb[16];
-#pragma unroll
-    for (int o = 0; o < 16; ++o) tb[o] = 0;
-    for (int c = tid; c < nch; c += NT) {
-        const int k = c / cpp;
-        if (k >= P) break; /* the zero pad chunk past n */
-        const uint4 pv = *reinterpret_cast<const uint4*>(pk + 16 * k);
-        const uint4 u = reinterpret_cast<const uint4*>(zz)[2 * c], v = reinterpret_cast<const uint4*>(zz)[2 * c + 1];
-        const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
-#pragma unroll
-        for (int o = 0; o < 16; ++o) {
-            if (o >= ro && o <= oo) {
-                const uint32_t p = (pw[o >> 2] >> (8 * (o & 3))) & 0xffu;
-                const uint32_t t = (u.x >> p) + (u.y >> p) + (u.z >> p) + (u.w >> p) + (v.x >> p) + (v.y >> p) +
-                                   (v.z >> p) + (v.w >> p);
-                tb[o] += t;
-            }
-        }
-    }
-#pragma unroll
-    for (int o = 0; o < 16; ++o) {
+}
+
+/* data bits of one chunk for every candidate order (chunk sum < 2^30 for narrow values) */
+__device__ __forceinline__ void chunk_rice_bits(const uint32_t (&z)[8], uint4 pv, int ro, int oo,
+                                                uint32_t (&tb)[16]) {
+    const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+    static_for<16>([&](auto O_) {
+        constexpr int o = O_;
         if (o >= ro && o <= oo) {
-            const uint64_t w = wave_sum_u64(tb[o]);
-            if (lane == 0) red[wid * 16 + o] = w;
+            const uint32_t p = (pw[o >> 2] >> (8 * (o & 3))) & 0xffu;
+            tb[o] += (z[0] >> p) + (z[1] >> p) + (z[2] >> p) + (z[3] >> p) + (z[4] >> p) + (z[5] >> p) +
+                     (z[6] >> p) + (z[7] >> p);
         }
+    });
+}
+
+/* reduce the per-thread data bits (each < 2^32), pick the order, write meta and parameters */
+__device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta* meta, const Decision* dec,
+                                            const uint32_t (&tb)[16], unsigned long long* rb,
+                                            unsigned long long* red, int* misc, const uint8_t* pk, int n,
+                                            int start, int rmin, int omax, int tid, int NT, int lane, int wid,
+                                            int nw, int64_t gid) {
+    const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+    uint32_t any = 0;
+#pragma unroll
+    for (int o = 0; o < 16; ++o) any |= (o >= ro && o <= oo) ? tb[o] : 0u;
+    if (__ballot(any >= (1u << 26)) == 0) { /* every lane < 2^26: the wave totals fit 32 bits */
+#pragma unroll
+        for (int o = 0; o < 16; ++o)
+            if (o >= ro && o <= oo) {
+                const uint32_t w = wave_sum_u32(tb[o]);
+                if (lane == 0) red[wid * 16 + o] = w;
+            }
+    } else {
+#pragma unroll
+        for (int o = 0; o < 16; ++o)
+            if (o >= ro && o <= oo) {
+                const uint64_t w = wave_sum_u64(tb[o]);
+                if (lane == 0) red[wid * 16 + o] = w;
+            }
     }
     __syncthreads();
     if (tid == 0) {
@@ -377,16 +374,17 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (n % (1 << o) == 0) rmax_eff = o;
+    const bool regz = resid_regz(n, rmax_eff, !WIDE && sizeof(ResT) == 4);
     const ResidLds lay = resid_lds_layout(LMAX, n, nw, 1 << (rmax_eff < 0 ? 0 : rmax_eff), S16 ? 2 : 4,
-                                          (int)sizeof(ResT), CT::BYTES);
+                                          (int)sizeof(ResT), CT::BYTES, regz);
     int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
     int32_t* xs32 = reinterpret_cast<int32_t*>(smem + lay.xs) + HP; /* [-HP, npad) (others) */
-    ResT* zz = reinterpret_cast<ResT*>(smem + lay.zz);              /* [npad] */
+    ResT* zz = reinterpret_cast<ResT*>(smem + lay.zz);              /* [npad] (LDS-resident mode) */
+    uint32_t* cs = reinterpret_cast<uint32_t*>(smem + lay.cs);       /* [nch] (register-resident mode) */
     uint32_t* cpair = reinterpret_cast<uint32_t*>(smem + lay.coef);  /* [LMAX][PPAD] */
     int32_t* cfl = reinterpret_cast<int32_t*>(smem + lay.coef + 4 * LMAX * CT::PPAD); /* [LMAX][CPAD] */
-    int32_t* lsh = cfl + LMAX * CT::CPAD; /* [4*LMAX] shift, start, -(2^shift), 2^(31-shift) */
+    int32_t* lsh = cfl + LMAX * CT::CPAD; /* [3*LMAX] shift, start, 2^(31-shift) */
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + lay.red);
-    unsigned long long* tot = reinterpret_cast<unsigned long long*>(smem + lay.tot);
     Decision* dec = reinterpret_cast<Decision*>(smem + lay.dec);
     unsigned long long* rb = reinterpret_cast<unsigned long long*>(smem + lay.rb);
     int* misc = reinterpret_cast<int*>(smem + lay.misc);
@@ -438,19 +436,20 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
             const int pp = i / CT::CPAD + 1, j = i % CT::CPAD;
             cfl[i] = (pp <= L && j < pp) ? rec[2 + L + (pp * (pp - 1)) / 2 + j] : 0;
         }
+        /* pair t of order pp: (lo = c[2t], hi = c[2t-1]) with c[-1] = -2^shift (S16 path) */
         for (int i = tid; i < LMAX * CT::PPAD; i += NT) {
             const int pp = i / CT::PPAD + 1, t = i % CT::PPAD;
             const int32_t* cp = rec + 2 + L + (pp * (pp - 1)) / 2;
-            const int32_t hi = (pp <= L && 2 * t < pp) ? cp[2 * t] : 0;
-            const int32_t lo = (pp <= L && 2 * t + 1 < pp) ? cp[2 * t + 1] : 0;
+            const int32_t lo = (pp <= L && 2 * t < pp) ? cp[2 * t] : 0;
+            const int32_t hi = (pp <= L && t >= 1 && 2 * t - 1 < pp) ? cp[2 * t - 1]
+                               : (pp <= L && t == 0) ? -(1 << rec[2 + pp - 1]) : 0;
             cpair[i] = ((uint32_t)hi << 16) | ((uint32_t)lo & 0xffffu);
         }
         for (int i = tid; i < LMAX; i += NT) {
             const int sh = i < L ? rec[2 + i] : 0; /* 0..15 */
             lsh[i] = sh;
             lsh[LMAX + i] = ((negmask >> i) & 1) ? 0 : i + 1; /* first residual index */
-            lsh[2 * LMAX + i] = -(1 << sh);
-            lsh[3 * LMAX + i] = (int32_t)(1u << (31 - sh));
+            lsh[2 * LMAX + i] = (int32_t)(1u << (31 - sh));
         }
     }
     if (tid == 0) {
@@ -495,75 +494,112 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         return;
     }
     /* ---- phase C: workgroup reduction ---- */
+    {
+        bool narrow = false;
+        if constexpr (!WIDE) {
+            uint32_t any = 0;
 #pragma unroll
-    for (int s = 0; s < NSUM; ++s) {
-        const uint64_t v = wave_sum_u64((uint64_t)acc[s]);
-        if (lane == 0) red[wid * NSUM + s] = v;
-    }
-    __syncthreads();
-    for (int s = tid; s < NSUM; s += NT) {
-        unsigned long long v = 0;
-        for (int w2 = 0; w2 < nw; ++w2) v += red[w2 * NSUM + s];
-        tot[s] = v;
+            for (int s = 0; s < NSUM; ++s) any |= acc[s];
+            narrow = __ballot(any >= (1u << 26)) == 0; /* every partial < 2^26: wave totals fit 32 bits */
+        }
+        if (narrow) {
+#pragma unroll
+            for (int s = 0; s < NSUM; ++s) {
+                const uint32_t v = wave_sum_u32((uint32_t)acc[s]);
+                if (lane == 0) red[wid * NSUM + s] = v;
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < NSUM; ++s) {
+                const uint64_t v = wave_sum_u64((uint64_t)acc[s]);
+                if (lane == 0) red[wid * NSUM + s] = v;
+            }
+        }
     }
     __syncthreads();
 
-    /* ---- phase D: choice (encoder.py:331-359, 398-404, 135-157) ---- */
-    if (tid == 0) {
-        Decision& d = *dec;
-        d.status = ST_OK;
-        d.site = 0;
+    /* ---- phase D: choice (encoder.py:331-359, 398-404, 135-157) by wave 0; lane j holds
+     * total j (fixed orders 0..4, then LPC orders 1..L) ---- */
+    if (wid == 0) {
+        uint64_t tj = 0;
+        if (lane < NSUM)
+            for (int w2 = 0; w2 < nw; ++w2) tj += red[w2 * NSUM + lane];
+        const uint32_t tlo = (uint32_t)tj, thi = (uint32_t)(tj >> 32);
+        auto tot_at = [&](int j) __attribute__((always_inline)) -> uint64_t {
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thi, j) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)tlo, j);
+        };
         int fo = 0;
-        if (n > 4)
-            for (int o = 1; o < 5; ++o)
-                if (tot[o] < tot[fo]) fo = o;
-        d.fixed_order = fo;
-        d.fixed_sum = (long long)tot[fo];
-        d.kind = FLACMI_KIND_FIXED;
-        d.order = fo;
-        d.shift = 0;
-        d.ncoefs = 0;
-        d.lpc_order = 0;
-        d.lpc_sum = 0;
-        for (int j = 0; j < FLACMI_MAX_LPC_ORDER; ++j) d.coef[j] = j < 4 ? c_fixed_coef[fo][j] : 0;
-        if (rice_only) {
-            d.fixed_order = 0;
-            d.fixed_sum = 0;
-            d.order = a.rice_order; /* identity "predictor": the row already is the residual */
-            for (int j = 0; j < 4; ++j) d.coef[j] = 0;
-        }
-        if (do_lpc) {
-            int best = 1;
-            for (int pp = 2; pp <= L; ++pp)
-                if (tot[4 + pp] < tot[4 + best]) best = pp;
-            d.lpc_order = best;
-            d.lpc_sum = (long long)tot[4 + best];
-            if (a.mode == FLACMI_MODE_LPC_ONLY) {
-                d.kind = FLACMI_KIND_LPC;
-                d.order = best;
-                d.shift = lsh[best - 1];
-                d.ncoefs = lsh[LMAX + best - 1] == 0 ? 0 : best;
-                for (int j = 0; j < FLACMI_MAX_LPC_ORDER; ++j)
-                    d.coef[j] = j < best ? cfl[(best - 1) * CT::CPAD + j] : 0;
-            } else if (tot[4 + best] < tot[fo]) {
-                /* A coefficient-less candidate (negative-shift branch) sums |x| over all n
-                 * samples, exactly the fixed order-0 sum, so it never gets here. */
-                d.kind = FLACMI_KIND_LPC;
-                d.order = best;
-                d.shift = lsh[best - 1];
-                d.ncoefs = best;
-                for (int j = 0; j < best; ++j) d.coef[j] = cfl[(best - 1) * CT::CPAD + j];
-            } else if (!(tot[fo] < tot[4 + best])) {
-                d.status = ST_ASSERT;
-                d.site = FLACMI_SITE_CHOICE_TIE;
+        uint64_t fsum = tot_at(0);
+        if (n > 4) {
+#pragma unroll
+            for (int o = 1; o < 5; ++o) {
+                const uint64_t v = tot_at(o);
+                if (v < fsum) {
+                    fsum = v;
+                    fo = o;
+                }
             }
         }
-        if (a.fixed_sums) {
-            for (int o = 0; o < 5; ++o) a.fixed_sums[gid * 5 + o] = (n > 4 || o == 0) ? (long long)tot[o] : 0;
+        int kind = FLACMI_KIND_FIXED, dorder = fo, dshift = 0, ncoefs = 0, lbest = 0, st = ST_OK, site = 0;
+        uint64_t lsum = 0;
+        if (rice_only) {
+            fo = 0;
+            fsum = 0;
+            dorder = a.rice_order; /* identity "predictor": the row already is the residual */
         }
+        if (do_lpc) {
+            lbest = 1;
+            lsum = tot_at(5);
+            static_for<LMAX>([&](auto P_) {
+                constexpr int pp = P_ + 1;
+                if (pp >= 2 && pp <= L) {
+                    const uint64_t v = tot_at(4 + pp);
+                    if (v < lsum) {
+                        lsum = v;
+                        lbest = pp;
+                    }
+                }
+            });
+            if (a.mode == FLACMI_MODE_LPC_ONLY) {
+                kind = FLACMI_KIND_LPC;
+                dorder = lbest;
+                dshift = lsh[lbest - 1];
+                ncoefs = lsh[LMAX + lbest - 1] == 0 ? 0 : lbest;
+            } else if (lsum < fsum) {
+                /* A coefficient-less candidate (negative-shift branch) sums |x| over all n
+                 * samples, exactly the fixed order-0 sum, so it never gets here. */
+                kind = FLACMI_KIND_LPC;
+                dorder = lbest;
+                dshift = lsh[lbest - 1];
+                ncoefs = lbest;
+            } else if (!(fsum < lsum)) {
+                st = ST_ASSERT;
+                site = FLACMI_SITE_CHOICE_TIE;
+            }
+        }
+        if (lane == 0) {
+            dec->status = st;
+            dec->site = site;
+            dec->kind = kind;
+            dec->order = dorder;
+            dec->shift = dshift;
+            dec->ncoefs = ncoefs;
+            dec->fixed_order = fo;
+            dec->lpc_order = lbest;
+            dec->fixed_sum = (long long)fsum;
+            dec->lpc_sum = (long long)lsum;
+        }
+        if (lane < FLACMI_MAX_LPC_ORDER) {
+            int cv = 0;
+            if (kind == FLACMI_KIND_LPC) cv = lane < lbest ? cfl[(lbest - 1) * CT::CPAD + lane] : 0;
+            else if (!rice_only && lane < 4) cv = c_fixed_coef[fo][lane];
+            dec->coef[lane] = cv;
+        }
+        if (a.fixed_sums && lane < 5) a.fixed_sums[gid * 5 + lane] = (n > 4 || lane == 0) ? (long long)tj : 0;
         if (a.lpc_sums) {
-            for (int pp = 1; pp <= 32; ++pp)
-                a.lpc_sums[gid * 32 + pp - 1] = (do_lpc && pp <= L) ? (long long)tot[4 + pp] : 0;
+            const uint64_t v = (uint64_t)__shfl((unsigned long long)tj, (lane + 5) & 63);
+            if (lane < 32) a.lpc_sums[gid * 32 + lane] = (do_lpc && lane + 1 <= L) ? (long long)v : 0;
         }
     }
     __syncthreads();
@@ -580,88 +616,162 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     const int start = (dec->kind == FLACMI_KIND_LPC && dec->ncoefs == 0) ? 0 : order;
     constexpr int TAPS = LMAX > 4 ? LMAX : 4;
 
-    /* ---- phase E: chosen residual, zig-zag, to LDS and HBM ---- */
+    /* ---- phase E: chosen residual, zig-zag, to HBM and to registers or LDS ---- */
     int wide_flag = 0;
     ResT* __restrict__ rout = reinterpret_cast<ResT*>(a.residual) + gid * a.residual_stride;
-    {
-        int32_t cf[TAPS];
+    int32_t cf[TAPS];
 #pragma unroll
-        for (int j = 0; j < TAPS; ++j) cf[j] = dec->coef[j];
-#pragma unroll 1
-        for (int c = tid; c < nch; c += NT) {
-            const int i0 = 8 * c;
-            int32_t w[HP + 8];
-            if constexpr (S16) {
-                const uint4* src = reinterpret_cast<const uint4*>(xs16 + i0 - HP);
+    for (int j = 0; j < TAPS; ++j) cf[j] = dec->coef[j];
+    auto resid_chunk = [&](int c, ResT (&zv)[8]) __attribute__((always_inline)) {
+        const int i0 = 8 * c;
+        int32_t w[HP + 8];
+        if constexpr (S16) {
+            const uint4* src = reinterpret_cast<const uint4*>(xs16 + i0 - HP);
 #pragma unroll
-                for (int g = 0; g < (HP + 8) / 8; ++g) {
-                    const uint4 v = src[g];
-                    const uint32_t q4[4] = {v.x, v.y, v.z, v.w};
+            for (int g = 0; g < (HP + 8) / 8; ++g) {
+                const uint4 v = src[g];
+                const uint32_t q4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        w[8 * g + 2 * e] = (int32_t)(int16_t)(q4[e] & 0xffff);
-                        w[8 * g + 2 * e + 1] = (int32_t)q4[e] >> 16;
-                    }
+                for (int e = 0; e < 4; ++e) {
+                    w[8 * g + 2 * e] = (int32_t)(int16_t)(q4[e] & 0xffff);
+                    w[8 * g + 2 * e + 1] = (int32_t)q4[e] >> 16;
                 }
+            }
+        } else {
+            const int4v* src = reinterpret_cast<const int4v*>(xs32 + i0 - HP);
+#pragma unroll
+            for (int g = 0; g < (HP + 8) / 4; ++g) {
+                const int4v v = src[g];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w[4 * g + e] = v[e];
+            }
+        }
+        static_for<8>([&](auto K_) {
+            constexpr int k = K_;
+            int64_t r;
+            if constexpr (!WIDE) {
+                int32_t pred = 0;
+                if (order <= 4) {
+                    static_for<4>([&](auto J_) { pred += sext24(cf[J_]) * sext24(w[HP + k - 1 - J_]); });
+                } else {
+                    static_for<TAPS>([&](auto J_) { pred += sext24(cf[J_]) * sext24(w[HP + k - 1 - J_]); });
+                }
+                r = (int64_t)(w[HP + k] - (pred >> dshift));
             } else {
-                const int4v* src = reinterpret_cast<const int4v*>(xs32 + i0 - HP);
-#pragma unroll
-                for (int g = 0; g < (HP + 8) / 4; ++g) {
-                    const int4v v = src[g];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) w[4 * g + e] = v[e];
-                }
+                int64_t pred = 0;
+                static_for<TAPS>([&](auto J_) { pred += (int64_t)cf[J_] * (int64_t)w[HP + k - 1 - J_]; });
+                r = (int64_t)w[HP + k] - (pred >> dshift);
             }
-            ResT zv[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                int64_t r;
-                if constexpr (!WIDE) {
-                    int32_t pred = 0;
-                    if (order <= 4) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) pred += sext24(cf[j]) * sext24(w[HP + k - 1 - j]);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < TAPS; ++j) pred += sext24(cf[j]) * sext24(w[HP + k - 1 - j]);
-                    }
-                    r = (int64_t)(w[HP + k] - (pred >> dshift));
-                } else {
-                    int64_t pred = 0;
-#pragma unroll
-                    for (int j = 0; j < TAPS; ++j) pred += (int64_t)cf[j] * (int64_t)w[HP + k - 1 - j];
-                    r = (int64_t)w[HP + k] - (pred >> dshift);
-                }
-                const int i = i0 + k;
-                ResT z;
-                if constexpr (sizeof(ResT) == 4) {
-                    if (WIDE && !(r >= -(1LL << 31) && r < (1LL << 31)) && i >= start && i < n) wide_flag = 1;
-                    const int32_t r32 = (int32_t)r;
-                    z = (ResT)(((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31));
-                } else {
-                    z = (ResT)(((uint64_t)r << 1) ^ (uint64_t)(r >> 63));
-                }
-                zv[k] = (i >= start && i < n) ? z : (ResT)0;
-            }
+            const int i = i0 + k;
+            ResT z;
             if constexpr (sizeof(ResT) == 4) {
-                const uint4 lo{zv[0], zv[1], zv[2], zv[3]}, hi{zv[4], zv[5], zv[6], zv[7]};
-                reinterpret_cast<uint4*>(zz + i0)[0] = lo;
-                reinterpret_cast<uint4*>(zz + i0)[1] = hi;
-                if (i0 + 8 <= n) {
-                    reinterpret_cast<uint4*>(rout + i0)[0] = lo;
-                    reinterpret_cast<uint4*>(rout + i0)[1] = hi;
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k)
-                        if (i0 + k < n) rout[i0 + k] = zv[k];
-                }
+                if (WIDE && !(r >= -(1LL << 31) && r < (1LL << 31)) && i >= start && i < n) wide_flag = 1;
+                const int32_t r32 = (int32_t)r;
+                z = (ResT)(((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31));
+            } else {
+                z = (ResT)(((uint64_t)r << 1) ^ (uint64_t)(r >> 63));
+            }
+            zv[k] = (i >= start && i < n) ? z : (ResT)0;
+        });
+    };
+    auto store_chunk = [&](int c, const ResT (&zv)[8]) __attribute__((always_inline)) {
+        const int i0 = 8 * c;
+        if constexpr (sizeof(ResT) == 4) {
+            if (i0 + 8 <= n) {
+                reinterpret_cast<uint4*>(rout + i0)[0] = uint4{zv[0], zv[1], zv[2], zv[3]};
+                reinterpret_cast<uint4*>(rout + i0)[1] = uint4{zv[4], zv[5], zv[6], zv[7]};
             } else {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    zz[i0 + k] = zv[k];
+                for (int k = 0; k < 8; ++k)
                     if (i0 + k < n) rout[i0 + k] = zv[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (i0 + k < n) rout[i0 + k] = zv[k];
+        }
+    };
+    auto lpc_only_done = [&]() __attribute__((always_inline)) {
+        if (tid == 0) {
+            put_meta(meta, ST_OK, 0, dec, 1);
+            meta->res_offset = start;
+            meta->res_len = n - start;
+            meta->part_order = -1;
+        }
+    };
+    auto first_order = [&]() __attribute__((always_inline)) {
+        int om = -1;
+        for (int o = a.rmin; o <= a.rmax; ++o)
+            if ((n % (1 << o)) == 0 && (n >> o) > order) om = o;
+        return om;
+    };
+
+    if constexpr (!WIDE && sizeof(ResT) == 4) {
+        if (regz) {
+            /* register-resident residual: chunk c = tid + j*NT, j < kCPT */
+            uint32_t zr[kCPT][8];
+#pragma unroll
+            for (int j = 0; j < kCPT; ++j) {
+                const int c = tid + j * NT;
+                if (c < nch) {
+                    resid_chunk(c, zr[j]);
+                    store_chunk(c, zr[j]);
+                    cs[c] = zr[j][0] + zr[j][1] + zr[j][2] + zr[j][3] + zr[j][4] + zr[j][5] + zr[j][6] + zr[j][7];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) zr[j][k] = 0;
                 }
             }
+            __syncthreads();
+            if (a.stop_after == 4) return;
+            if (a.mode == FLACMI_MODE_LPC_ONLY) {
+                lpc_only_done();
+                return;
+            }
+            /* ---- phase F (register-resident) ---- */
+            const int omax = first_order();
+            if (omax < 0) {
+                if (tid == 0) put_meta(meta, ST_ASSERT, FLACMI_SITE_RICE_NO_ORDER, dec, 1);
+                return;
+            }
+            const int cpp = (n >> omax) >> 3; /* chunks per finest partition */
+            uint8_t* pk = reinterpret_cast<uint8_t*>(hs);
+            if (wid == 0) {
+                uint64_t s = 0;
+                if (lane < (1 << omax))
+                    for (int c = lane * cpp; c < (lane + 1) * cpp; ++c) s += cs[c];
+                rice_params_wave0(a, s, tl, rb, misc, pk, n, order, a.rmin, omax, lane);
+            }
+            __syncthreads();
+            if (misc[0] >= 0) {
+                if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
+                return;
+            }
+            const int ro = __builtin_amdgcn_readfirstlane(a.rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+            uint32_t tb[16];
+#pragma unroll
+            for (int o = 0; o < 16; ++o) tb[o] = 0;
+#pragma unroll
+            for (int j = 0; j < kCPT; ++j) {
+                const int c = tid + j * NT;
+                if (c < nch) chunk_rice_bits(zr[j], *reinterpret_cast<const uint4*>(pk + 16 * (c / cpp)), ro, oo, tb);
+            }
+            rice_finish(a, meta, dec, tb, rb, red, misc, pk, n, start, a.rmin, omax, tid, NT, lane, wid, nw, gid);
+            return;
+        }
+    }
+
+#pragma unroll 1
+    for (int c = tid; c < nch; c += NT) {
+        ResT zv[8];
+        resid_chunk(c, zv);
+        store_chunk(c, zv);
+        if constexpr (sizeof(ResT) == 4) {
+            reinterpret_cast<uint4*>(zz + 8 * c)[0] = uint4{zv[0], zv[1], zv[2], zv[3]};
+            reinterpret_cast<uint4*>(zz + 8 * c)[1] = uint4{zv[4], zv[5], zv[6], zv[7]};
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) zz[8 * c + k] = zv[k];
         }
     }
     if (wide_flag) misc[2] = 1;
@@ -672,30 +782,49 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         return;
     }
     if (a.mode == FLACMI_MODE_LPC_ONLY) {
-        if (tid == 0) {
-            put_meta(meta, ST_OK, 0, dec, 1);
-            meta->res_offset = start;
-            meta->res_len = n - start;
-            meta->part_order = -1;
-        }
+        lpc_only_done();
         return;
     }
 
     /* ---- phase F: Rice partition search (encoder.py:655-760) ---- */
-    int omax = -1;
-    for (int o = a.rmin; o <= a.rmax; ++o)
-        if ((n % (1 << o)) == 0 && (n >> o) > order) omax = o;
+    const int omax = first_order();
     if (omax < 0) {
         if (tid == 0) put_meta(meta, ST_ASSERT, FLACMI_SITE_RICE_NO_ORDER, dec, 1);
         return;
     }
     const int rmin = a.rmin;
     const int P = 1 << omax, ps = n >> omax;
-    if constexpr (!WIDE) {
+    if constexpr (!WIDE && sizeof(ResT) == 4) {
         /* zz < 2^27 here, so a chunk of eight fits 32 bits */
-        if ((ps & 7) == 0 && P <= 64) {
-            rice_search_fast(a, meta, dec, zz, tl, rb, red, misc, reinterpret_cast<uint8_t*>(hs), n, order, start,
-                             rmin, omax, nch, tid, NT, lane, wid, nw, gid);
+        if ((ps & 7) == 0 && P <= 64 && 8 * kCPT * NT >= n) {
+            const int cpp = ps >> 3;
+            uint8_t* pk = reinterpret_cast<uint8_t*>(hs);
+            if (wid == 0) {
+                uint64_t s = 0;
+                if (lane < P) {
+                    const uint4* z4 = reinterpret_cast<const uint4*>(zz + lane * ps);
+                    for (int c = 0; c < cpp; ++c) {
+                        const uint4 u = z4[2 * c], v = z4[2 * c + 1];
+                        s += (uint64_t)(u.x + u.y + u.z + u.w + v.x + v.y + v.z + v.w);
+                    }
+                }
+                rice_params_wave0(a, s, tl, rb, misc, pk, n, order, rmin, omax, lane);
+            }
+            __syncthreads();
+            if (misc[0] >= 0) {
+                if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
+                return;
+            }
+            const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+            uint32_t tb[16];
+#pragma unroll
+            for (int o = 0; o < 16; ++o) tb[o] = 0;
+            for (int c = tid; c < nch; c += NT) {
+                const uint4 u = reinterpret_cast<const uint4*>(zz)[2 * c], v = reinterpret_cast<const uint4*>(zz)[2 * c + 1];
+                const uint32_t z[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                chunk_rice_bits(z, *reinterpret_cast<const uint4*>(pk + 16 * (c / cpp)), ro, oo, tb);
+            }
+            rice_finish(a, meta, dec, tb, rb, red, misc, pk, n, start, rmin, omax, tid, NT, lane, wid, nw, gid);
             return;
         }
     }
@@ -802,8 +931,10 @@ static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
     const int nt = resid_threads(a.n);
+    const bool regz = resid_regz(a.n, rmax_eff, PATH != PATH_W64 && sizeof(ResT) == 4);
     const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff),
-                                        PATH == PATH_S16 ? 2 : 4, (int)sizeof(ResT), CoefTables<LMAX>::BYTES).total;
+                                        PATH == PATH_S16 ? 2 : 4, (int)sizeof(ResT), CoefTables<LMAX>::BYTES,
+                                        regz).total;
     auto kern = k_resid<LMAX, PATH, ResT>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
