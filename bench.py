@@ -92,6 +92,30 @@ def cpu_baseline(cfg, seconds, seed):
                       f"Python itself measured 56.8k samples/s/core here (BASELINE.md)"}
 
 
+def shard_first_unit(rank, units_per_rank):
+    """First global unit of a rank's shard: contiguous, disjoint block ranges (units are
+    independent), so the stream statistics are a plain sum over ranks."""
+    return rank * units_per_rank
+
+
+def reduce_stats(stats, dist=None):
+    """Stream totals over ranks: the one collective of the multi-GPU path (RCCL over xGMI
+    on the GPU; the gloo CPU tests exercise the same call)."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(stats)
+    return stats
+
+
+def reduce_elapsed(elapsed, dist=None, device=None):
+    """Max over ranks of the timed region (the contract's whole-job time)."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+    return elapsed
+
+
 def main():
     args = parse()
     cfg = dict(CONFIGS[args.config])
@@ -123,7 +147,7 @@ def main():
     sstride = ((n * sbytes + 15) // 16) * 16 // sbytes
     rstride = ((n * 4 + 15) // 16) * 16 // 4
     pstride = params_stride_for(cfg["rmax"])
-    first_unit = rank * units  # contiguous shard of the global unit space (units are independent)
+    first_unit = shard_first_unit(rank, units)
 
     samples = torch.empty((units, sstride), dtype=sdt, device=dev)
     meta = torch.empty((units, abi.META_DTYPE.itemsize), dtype=torch.uint8, device=dev)
@@ -137,8 +161,7 @@ def main():
         az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, units, n, params, meta.data_ptr(),
                           rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, sptr)
         az.stream_stats(meta.data_ptr(), units, n, stats.data_ptr(), sptr)
-        if distributed:
-            dist.all_reduce(stats)  # RCCL over xGMI: the only collective (stream totals)
+        reduce_stats(stats, dist)
 
     for _ in range(args.warmup):
         step()
@@ -156,10 +179,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kt = az.timing()
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = reduce_elapsed(elapsed, dist, dev)
 
     meta_np = meta.cpu().numpy().view(abi.META_DTYPE).reshape(units)
     st = stats.cpu().numpy()

@@ -183,29 +183,37 @@ __host__ __device__ inline bool resid_regz(int n, int rmax_eff, bool narrow32) {
 
 /* LDS layout of k_resid: byte offsets (multiples of 16) from the dynamic LDS base.  The
  * host sizes the allocation with the same function the kernel carves it with. */
+/* MFMA candidate-sum planes (k_resid, S16 path): bf16 high / low sample bytes, elements
+ * [-16, len - 16) per plane. */
+__host__ __device__ inline int mfma_plane_len(int n) { return ((n + 63) / 64) * 64 + 32; }
+
 struct ResidLds {
-    int xs, zz, cs, coef, red, dec, rb, misc, hs, hp, tl, total;
+    int xs, pl, zz, cs, coef, red, dec, rb, misc, hs, hp, tl, total;
 };
 /* floor(log2) thresholds staged in LDS for exponents [kTlLo, kTlLo + 64): every Rice
  * mean S/len of a 32-bit residual (S >= 1, len <= 65535, S < 2^48) falls inside. */
 constexpr int kTlLo = -16;
 __host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, int P, int xbytes, int zbytes,
-                                                     int coef_bytes, bool regz) {
+                                                     int coef_bytes, bool regz, bool planes) {
     auto up = [](int b) { return (b + 15) & ~15; };
     const int nsum = 5 + lmax;
     const int npad = ((n + 7) / 8) * 8 + 8;
     ResidLds l;
     int o = 0;
     l.xs = o;   o = up(o + xbytes * (resid_hp(lmax) + npad));
+    /* the MFMA planes are dead after the candidate sums; the residual-side regions reuse them */
+    l.pl = o;
+    const int pl_end = up(o + (planes ? 2 * 2 * mfma_plane_len(n) : 0));
     l.zz = o;   o = up(o + (regz ? 0 : zbytes * npad)); /* zig-zag row (LDS-resident mode) */
     l.cs = o;   o = up(o + (regz ? 4 * (npad / 8) : 0)); /* chunk sums (register-resident mode) */
+    l.hs = o;   o = up(o + 8 * 2 * P);
+    l.hp = o;   o = up(o + 4 * 2 * P);
+    o = o > pl_end ? o : pl_end;
     l.coef = o; o = up(o + coef_bytes);
     l.red = o;  o = up(o + 8 * nw * (nsum > 16 ? nsum : 16));
     l.dec = o;  o = up(o + (int)sizeof(Decision));
     l.rb = o;   o = up(o + 8 * 32);
     l.misc = o; o = up(o + 4 * 8);
-    l.hs = o;   o = up(o + 8 * 2 * P);
-    l.hp = o;   o = up(o + 4 * 2 * P);
     l.tl = o;   o = up(o + 8 * 64);
     l.total = o;
     return l;

@@ -298,6 +298,15 @@ static int debug_stop() {
     return v;
 }
 
+/* FLACMI_NO_MFMA=1 keeps the candidate sums on the VALU path (comparison runs). */
+static int use_mfma() {
+    static const int v = [] {
+        const char* e = getenv("FLACMI_NO_MFMA");
+        return (e && atoi(e) != 0) ? 0 : 1;
+    }();
+    return v;
+}
+
 static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi_params* p,
                                const flacmi_outputs* o, hipStream_t s) {
     if (int rc = set_device(ctx)) return rc;
@@ -367,6 +376,7 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.fixed_sums = o->fixed_sums ? o->fixed_sums + cls[c].unit0 * 5 : nullptr;
         a.lpc_sums = o->lpc_sums ? o->lpc_sums + cls[c].unit0 * 32 : nullptr;
         a.stop_after = debug_stop();
+        a.mfma = use_mfma();
         const bool wide = needs_wide(cls[c].n, b->sample_bits, L, p->qlp_precision, p->mode);
         const int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
         HIP_TRY(launch_resid(a, path, o->residual_bytes, s));

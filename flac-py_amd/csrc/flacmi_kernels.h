@@ -45,6 +45,7 @@ struct ResidArgs {
     int32_t stop_after;      /* profiling ablation (env FLACMI_DEBUG_STOP): 0 = full kernel,
                                 1 = after staging, 2 = after candidate sums, 3 = after the
                                 choice, 4 = after the chosen residual */
+    int32_t mfma;            /* 1 = MFMA candidate sums where exact (env FLACMI_NO_MFMA=1 -> 0) */
 };
 
 struct ResidLaunch {

@@ -111,7 +111,7 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes) {
     ResidLaunch r;
     r.threads = resid_threads(n);
     r.lds_bytes = resid_lds_layout(32, n, r.threads / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff), 4,
-                                   residual_bytes == 8 ? 8 : 4, 16 * 1024, false).total;
+                                   residual_bytes == 8 ? 8 : 4, 16 * 1024, false, true).total;
     return r;
 }
 

@@ -226,6 +226,134 @@ __device__ __forceinline__ void chunk_sums_32(const int32_t (&w)[HP + 8], int i0
     });
 }
 
+/* ---------------------------------------------------------------------------------------
+ * MFMA candidate sums (PATH_S16, L <= 12): one v_mfma_f32_16x16x32_bf16 computes, for 16
+ * samples and 16 predictors (LPC orders 1..12, fixed orders 1..4),
+ *     f = pred * 2^-sh - x[i] + (2^-(sh+1) - 1/2)         (C operand = the last term)
+ * from bf16 planes of the sample bytes, x = 256*h + l (h signed, l unsigned), so that
+ * floor(f + 1/2 - 2^-(sh+1)) = (pred >> sh) - x[i] = -r.  Every product and partial sum
+ * is a multiple of 2^-(sh+1) below 2^24 in magnitude when (sum|c| + 2^sh) * 33023 < 2^22,
+ * so the f32 accumulation is exact; the host-side bound check is per unit (phase A).
+ * Then w = f + 1.5*2^23 rounds to the integer floor and its bit pattern is
+ * 0x4B400000 + (-r): |r| is one v_sad_u32 accumulate.  Per sample and predictor: one
+ * v_add_f32 and one v_sad_u32, against ceil((p+1)/2) dots + shift + sad on the VALU.
+ *
+ * Block of 64 samples i0..i0+63, four MFMAs rho = 0..3: row s of MFMA rho is the sample
+ * i0 + 4s + rho; its 16-wide tap window is positions [i0 + 4s - 12, i0 + 4s + 4) (the same
+ * for every rho, so the A fragment is loaded once per block, 8-byte aligned), and B_rho
+ * places each predictor's taps at window offset d + 12 + rho for x[i + d].
+ * A fragment: lane l holds A[row l&15][k = 8(l>>4) + j]: k < 16 -> h plane, k >= 16 -> l
+ * plane, window element k mod 16.  D: lane l holds column l&15, rows 4(l>>4) + r.
+ * ------------------------------------------------------------------------------------- */
+typedef short frag_ab __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float frag_cd __attribute__((ext_vector_type(4)));
+constexpr uint32_t kFloorMagicBits = 0x4B400000u; /* 1.5 * 2^23 */
+constexpr float kFloorMagic = 12582912.0f;
+constexpr int kMfmaCoefLimit = 127; /* sum|c| + 2^sh; 127 * 33023 < 2^22 */
+
+__device__ __forceinline__ uint32_t bf16_hi(float v) { return __float_as_uint(v) & 0xffff0000u; }
+__device__ __forceinline__ uint32_t bf16_pack(float lo, float hi) {
+    return (__float_as_uint(lo) >> 16) | bf16_hi(hi);
+}
+
+/* v_sad_u32 acc + |a - b| as one instruction (the pattern match is lost on a constant b) */
+__device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t acc) {
+    asm("v_sad_u32 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+    return acc;
+}
+
+template <int LMAX, bool MASK>
+__device__ __forceinline__ uint32_t mfma_block(const uint16_t* pb, int i0, int eoff, const frag_ab (&B)[4],
+                                               const frag_cd& C, int kb, int start, int n, uint32_t mb) {
+    const uint2 a0 = *reinterpret_cast<const uint2*>(pb + i0 + eoff);
+    const uint2 a1 = *reinterpret_cast<const uint2*>(pb + i0 + eoff + 4);
+    const uint4 av{a0.x, a0.y, a1.x, a1.y};
+    const bf16x8 A = __builtin_bit_cast(bf16x8, av);
+    frag_cd D[4];
+    static_for<4>([&](auto R_) {
+        D[R_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, B[R_]), C, 0, 0, 0);
+    });
+    uint32_t bs[4] = {0, 0, 0, 0};
+    static_for<4>([&](auto R_) {
+        constexpr int rho = R_;
+        static_for<4>([&](auto Q_) {
+            constexpr int r = Q_;
+            const uint32_t wv = __float_as_uint(D[rho][r] + kFloorMagic);
+            if constexpr (MASK) {
+                const int i = i0 + 4 * (4 * kb + r) + rho;
+                const uint32_t t = sad_u32(wv, mb, 0u);
+                bs[r] += (i >= start && i < n) ? t : 0u;
+            } else {
+                bs[r] = sad_u32(wv, mb, bs[r]);
+            }
+        });
+    });
+    return bs[0] + bs[1] + bs[2] + bs[3];
+}
+
+/* Sums for the fixed orders 1..4 and LPC orders 1..min(L,12) into red[wid][.] (the order-0
+ * sum, sum|x|, comes from the staging pass). */
+template <int LMAX>
+__device__ __forceinline__ void mfma_candidate_sums(const uint16_t* Hp, const uint16_t* Lp, const int32_t* cfl,
+                                                    const int32_t* lsh, int L, int n, int lane, int wid, int nw,
+                                                    unsigned long long* red, uint32_t sumx) {
+    using CT = CoefTables<LMAX>;
+    constexpr int NSUM = 5 + LMAX;
+    const int col = lane & 15, kb = lane >> 4;
+    const bool lpc_col = col < 12;
+    int ncoef = 0, sh = 0, start = 0;
+    if (lpc_col) {
+        if (col + 1 <= L) {
+            sh = lsh[col];
+            start = lsh[LMAX + col];
+            ncoef = col + 1;
+        }
+    } else {
+        ncoef = col - 11;
+        start = ncoef;
+    }
+    const float scale = (kb >> 1) ? 1.0f : 256.0f;
+    const float inv = __uint_as_float((uint32_t)(127 - sh) << 23); /* 2^-sh */
+    frag_ab B[4];
+    static_for<4>([&](auto R_) {
+        constexpr int rho = R_;
+        static_for<8>([&](auto J_) {
+            constexpr int j = J_;
+            const int d = 8 * (kb & 1) + j - 12 - rho; /* tap x[i + d] */
+            float v = 0.0f;
+            if (d == 0) {
+                v = -scale;
+            } else if (d < 0 && -1 - d < ncoef) {
+                const int jj = -1 - d;
+                const int c = lpc_col ? cfl[col * CT::CPAD + jj] : c_fixed_coef[col - 11][jj];
+                v = scale * (float)c * inv;
+            }
+            B[rho][j] = (short)(__float_as_uint(v) >> 16);
+        });
+    });
+    const float cinit = 0.5f * inv - 0.5f;
+    const frag_cd C{cinit, cinit, cinit, cinit};
+    const uint16_t* pb = (kb >> 1) ? Lp : Hp;
+    const int eoff = 4 * (lane & 15) - 12 + 8 * (kb & 1);
+    uint64_t acc = 0;
+    const uint32_t mb = kFloorMagicBits;
+    const int nblk = (n + 63) >> 6;
+    for (int blk = wid; blk < nblk; blk += nw) {
+        const int i0 = blk << 6;
+        if (blk == 0 || i0 + 64 > n) acc += mfma_block<LMAX, true>(pb, i0, eoff, B, C, kb, start, n, mb);
+        else acc += mfma_block<LMAX, false>(pb, i0, eoff, B, C, kb, start, n, mb);
+    }
+    acc += (uint64_t)__shfl_xor((unsigned long long)acc, 16);
+    acc += (uint64_t)__shfl_xor((unsigned long long)acc, 32);
+    const uint32_t sx = wave_sum_u32(sumx);
+    if (lane < 16) {
+        const int si = lpc_col ? 5 + col : col - 11;
+        if (si < NSUM) red[wid * NSUM + si] = acc;
+    }
+    if (lane == 0) red[wid * NSUM] = sx;
+}
+
 /* floor(log2(x)) for a Rice mean x (normal, > 0): LDS thresholds, global table outside. */
 __device__ __forceinline__ int rice_floor_log2(double x, const double* tl, const double* gthr) {
     const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
@@ -357,6 +485,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     using CT = CoefTables<LMAX>;
     constexpr int HP = resid_hp(LMAX);
     constexpr int NSUM = 5 + LMAX;
+    constexpr bool MF = S16 && (LMAX == 8 || LMAX == 12); /* MFMA candidate sums available */
 
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, wid = tid >> 6, nw = NT >> 6;
@@ -376,7 +505,9 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         if (n % (1 << o) == 0) rmax_eff = o;
     const bool regz = resid_regz(n, rmax_eff, !WIDE && sizeof(ResT) == 4);
     const ResidLds lay = resid_lds_layout(LMAX, n, nw, 1 << (rmax_eff < 0 ? 0 : rmax_eff), S16 ? 2 : 4,
-                                          (int)sizeof(ResT), CT::BYTES, regz);
+                                          (int)sizeof(ResT), CT::BYTES, regz, MF);
+    uint16_t* Hp = reinterpret_cast<uint16_t*>(smem + lay.pl) + 16; /* bf16 high bytes [-16, plen-16) */
+    uint16_t* Lp = Hp + mfma_plane_len(n);                            /* bf16 low bytes */
     int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
     int32_t* xs32 = reinterpret_cast<int32_t*>(smem + lay.xs) + HP; /* [-HP, npad) (others) */
     ResT* zz = reinterpret_cast<ResT*>(smem + lay.zz);              /* [npad] (LDS-resident mode) */
@@ -395,6 +526,8 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     const int32_t* __restrict__ rec = ref_mode ? a.rec + gid * a.rec_words : nullptr;
 
     /* ---- phase A: stage samples and the candidate coefficients ---- */
+    uint32_t sumx = 0; /* this thread's sum|x| (MFMA path: the fixed order-0 sum) */
+    int mf_ok = 1;     /* this thread's orders pass the MFMA exactness bound */
     if (ref_mode) {
         const int st = rec[0];
         if (st != 0) { /* the reference raises inside encode_subframe_lpc */
@@ -407,9 +540,39 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         for (int i = n + tid; i < npad; i += NT) xs16[i] = 0;
         const int16_t* __restrict__ src = (const int16_t*)a.samples + u * a.stride;
         const int nv = n >> 3;
-        for (int v = tid; v < nv; v += NT)
-            *reinterpret_cast<uint4*>(xs16 + 8 * v) = *reinterpret_cast<const uint4*>(src + 8 * v);
-        for (int i = nv * 8 + tid; i < n; i += NT) xs16[i] = src[i];
+        if constexpr (MF) {
+            /* also the bf16 planes x = 256*h + l (h = x >> 8 signed, l = x & 255) and sum|x| */
+            const int plen = mfma_plane_len(n);
+            for (int i = tid; i < 16; i += NT) Hp[i - 16] = Lp[i - 16] = 0;
+            for (int i = n + tid; i < plen - 16; i += NT) Hp[i] = Lp[i] = 0;
+            for (int v = tid; v < nv; v += NT) {
+                const uint4 q = *reinterpret_cast<const uint4*>(src + 8 * v);
+                *reinterpret_cast<uint4*>(xs16 + 8 * v) = q;
+                const uint32_t qd[4] = {q.x, q.y, q.z, q.w};
+                uint32_t hw[4], lw[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t d = qd[e];
+                    const int32_t x0 = (int32_t)(d << 16) >> 16, x1 = (int32_t)d >> 16;
+                    hw[e] = bf16_pack((float)((int32_t)(d << 16) >> 24), (float)((int32_t)d >> 24));
+                    lw[e] = bf16_pack((float)(d & 0xffu), (float)((d >> 16) & 0xffu));
+                    sumx += (uint32_t)(x0 < 0 ? -x0 : x0) + (uint32_t)(x1 < 0 ? -x1 : x1);
+                }
+                *reinterpret_cast<uint4*>(Hp + 8 * v) = uint4{hw[0], hw[1], hw[2], hw[3]};
+                *reinterpret_cast<uint4*>(Lp + 8 * v) = uint4{lw[0], lw[1], lw[2], lw[3]};
+            }
+            for (int i = nv * 8 + tid; i < n; i += NT) {
+                const int32_t x = src[i];
+                xs16[i] = (int16_t)x;
+                Hp[i] = (uint16_t)(__float_as_uint((float)(x >> 8)) >> 16);
+                Lp[i] = (uint16_t)(__float_as_uint((float)(x & 0xff)) >> 16);
+                sumx += (uint32_t)(x < 0 ? -x : x);
+            }
+        } else {
+            for (int v = tid; v < nv; v += NT)
+                *reinterpret_cast<uint4*>(xs16 + 8 * v) = *reinterpret_cast<const uint4*>(src + 8 * v);
+            for (int i = nv * 8 + tid; i < n; i += NT) xs16[i] = src[i];
+        }
     } else {
         for (int i = tid; i < HP; i += NT) xs32[i - HP] = 0;
         for (int i = n + tid; i < npad; i += NT) xs32[i] = 0;
@@ -450,6 +613,12 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
             lsh[i] = sh;
             lsh[LMAX + i] = ((negmask >> i) & 1) ? 0 : i + 1; /* first residual index */
             lsh[2 * LMAX + i] = (int32_t)(1u << (31 - sh));
+            if (MF && i < L) {
+                const int32_t* cp = rec + 2 + L + (i * (i + 1)) / 2;
+                int sa = 1 << sh;
+                for (int j = 0; j <= i; ++j) sa += cp[j] < 0 ? -cp[j] : cp[j];
+                mf_ok &= sa <= kMfmaCoefLimit;
+            }
         }
     }
     if (tid == 0) {
@@ -459,10 +628,19 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     }
     if (tid < 32) rb[tid] = 0;
     if (tid < 64) tl[tid] = a.log2thr[tid + kTlLo + 1074];
-    __syncthreads();
+    bool use_mfma = false;
+    if constexpr (MF) {
+        use_mfma = __syncthreads_and(mf_ok) && do_lpc && a.mfma;
+    } else {
+        __syncthreads();
+    }
     if (a.stop_after == 1) return;
 
     /* ---- phase B: sum|r| for fixed orders 0..4 and LPC orders 1..L ---- */
+    if (use_mfma) {
+        if constexpr (MF) mfma_candidate_sums<LMAX>(Hp, Lp, cfl, lsh, L, n, lane, wid, nw, red, sumx);
+        if (a.stop_after == 2) return;
+    } else {
     A acc[NSUM];
 #pragma unroll
     for (int s = 0; s < NSUM; ++s) acc[s] = 0;
@@ -515,6 +693,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
                 if (lane == 0) red[wid * NSUM + s] = v;
             }
         }
+    }
     }
     __syncthreads();
 
@@ -934,7 +1113,7 @@ static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     const bool regz = resid_regz(a.n, rmax_eff, PATH != PATH_W64 && sizeof(ResT) == 4);
     const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff),
                                         PATH == PATH_S16 ? 2 : 4, (int)sizeof(ResT), CoefTables<LMAX>::BYTES,
-                                        regz).total;
+                                        regz, PATH == PATH_S16 && (LMAX == 8 || LMAX == 12)).total;
     auto kern = k_resid<LMAX, PATH, ResT>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

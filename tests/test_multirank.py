@@ -1,0 +1,84 @@
+"""N > 1 path on CPU: world_size-2 gloo ranks, each analysing its own contiguous shard of
+synthetic units (bench.shard_first_unit) through the oracle, then bench.reduce_stats /
+bench.reduce_elapsed over torch.distributed.  The all-reduced stream statistics must equal
+the single-process statistics of the whole unit range: the shards are disjoint, cover the
+range, and every statistic is a sum (no data-path collective)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+N, BITS, L, Q, RMIN, RMAX, SEED, U = 4608, 16, 12, 5, 0, 5, 2024, 6
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _shard_stats(rank):
+    for p in (REPO, os.path.join(REPO, "oracle"), HERE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import bench
+    import oracle
+    from stats_mirror import stream_stats
+    first = bench.shard_first_unit(rank, U)
+    a = oracle.synth_batch(first, U, N, BITS, SEED, dtype=np.int16)
+    r = oracle.analyze_batch(a, oracle.make_params(L, Q, RMIN, RMAX, 0), N, threads=2)
+    return stream_stats(r["meta"], N)
+
+
+def _worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    import bench
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        st = torch.from_numpy(_shard_stats(rank))
+        bench.reduce_stats(st, dist)
+        el = bench.reduce_elapsed(0.5 + rank, dist)
+        out.put((rank, st.numpy().tolist(), el))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_stats_equal_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process over the whole range [0, world*U)
+    sys.path[:0] = [REPO, os.path.join(REPO, "oracle"), HERE]
+    import oracle
+    from stats_mirror import stream_stats
+    a = oracle.synth_batch(0, world * U, N, BITS, SEED, dtype=np.int16)
+    r = oracle.analyze_batch(a, oracle.make_params(L, Q, RMIN, RMAX, 0), N, threads=4)
+    want = stream_stats(r["meta"], N).tolist()
+    for rank, st, el in res:
+        assert st == want, f"rank {rank}: all-reduced stats differ from the single-process stats"
+        assert el == 1.5  # max over ranks of 0.5 and 1.5
+    assert want[0] == world * U and want[1] == world * U * N
+
+
+def test_shards_disjoint_and_covering():
+    sys.path.insert(0, REPO)
+    import bench
+    for world in (1, 2, 4, 8):
+        spans = [(bench.shard_first_unit(r, 1000), bench.shard_first_unit(r, 1000) + 1000) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == world * 1000
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))

@@ -23,6 +23,16 @@ __global__ __launch_bounds__(256) void kern(int* out, int a0, int b0) {
         if constexpr (K == 6) { OP16("v_mul_lo_u32 %0, %1, %0") }
         if constexpr (K == 7) { OP16("v_pk_mad_i16 %0, %1, %2, %0") }
         if constexpr (K == 8) { OP16("v_lshrrev_b32 %0, %1, %0") }
+        if constexpr (K == 9) { OP16("v_floor_f32 %0, %0") }
+        if constexpr (K == 10) { OP16("v_cvt_i32_f32 %0, %0") }
+        if constexpr (K == 11) { OP16("v_cvt_u32_f32_e64 %0, |%0|") }
+        if constexpr (K == 12) { OP16("v_add_u32_e64 %0, %1, %0") }
+        if constexpr (K == 13) { OP16("v_cvt_flr_i32_f32 %0, %0") }
+        if constexpr (K == 14) { OP16("v_max_i32 %0, %1, %0") }
+        if constexpr (K == 15) { OP16("v_add_f32_e64 %0, |%1|, %0") }
+        if constexpr (K == 16) { OP16("v_xor_b32 %0, %1, %0") }
+        if constexpr (K == 17) { OP16("v_alignbit_b32 %0, %1, %0, 16") }
+        if constexpr (K == 18) { OP16("v_cndmask_b32 %0, %1, %0, vcc") }
     }
     int s = 0;
     for (int j = 0; j < 16; ++j) s += acc[j];
@@ -30,7 +40,9 @@ __global__ __launch_bounds__(256) void kern(int* out, int a0, int b0) {
 }
 
 static const char* names[] = {"v_add_u32", "v_dot2c_i32_i16", "v_mad_i32_i24", "v_sad_u32", "v_dot4c_i32_i8",
-                              "v_dot2_i32_i16 (vop3p)", "v_mul_lo_u32", "v_pk_mad_i16", "v_lshrrev_b32",
+                              "v_dot2_i32_i16 (vop3p)", "v_mul_lo_u32", "v_pk_mad_i16", "v_lshrrev_b32", "v_floor_f32",
+                              "v_cvt_i32_f32", "v_cvt_u32_f32_e64 |x|", "v_add_u32_e64", "v_cvt_flr_i32_f32",
+                              "v_max_i32", "v_add_f32_e64 |x|", "v_xor_b32", "v_alignbit_b32", "v_cndmask_b32",
                               "v_mad_u64_u32"};
 
 template <int K>
@@ -58,16 +70,21 @@ int main() {
     const int cus = p.multiProcessorCount;
     hipMalloc(&d, sizeof(int) * cus * 32 * 64 * 4);
     printf("CUs %d clock %d kHz\n", cus, p.clockRate);
-    for (int wpc : {8, 16}) {
+    for (int wpc : {16}) {
         run<0>(d, cus, wpc);
         run<1>(d, cus, wpc);
-        run<2>(d, cus, wpc);
         run<3>(d, cus, wpc);
-        run<4>(d, cus, wpc);
-        run<5>(d, cus, wpc);
-        run<6>(d, cus, wpc);
-        run<7>(d, cus, wpc);
         run<8>(d, cus, wpc);
+        run<9>(d, cus, wpc);
+        run<10>(d, cus, wpc);
+        run<11>(d, cus, wpc);
+        run<12>(d, cus, wpc);
+        run<13>(d, cus, wpc);
+        run<14>(d, cus, wpc);
+        run<15>(d, cus, wpc);
+        run<16>(d, cus, wpc);
+        run<17>(d, cus, wpc);
+        run<18>(d, cus, wpc);
     }
     hipFree(d);
     return 0;
