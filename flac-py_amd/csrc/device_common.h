@@ -183,6 +183,13 @@ __host__ __device__ inline bool resid_regz(int n, int rmax_eff, bool narrow32) {
 
 /* LDS layout of k_resid: byte offsets (multiples of 16) from the dynamic LDS base.  The
  * host sizes the allocation with the same function the kernel carves it with. */
+/* staged samples occupy [-HP, resid_xpad(n)): the 8-sample chunks plus one, and the
+ * 64-sample MFMA blocks; zero past n */
+__host__ __device__ inline int resid_xpad(int n) {
+    const int a = ((n + 7) / 8) * 8 + 8, b = ((n + 63) / 64) * 64 + 8;
+    return a > b ? a : b;
+}
+
 /* MFMA candidate-sum planes (k_resid, S16 path): bf16 high / low sample bytes, elements
  * [-16, len - 16) per plane. */
 __host__ __device__ inline int mfma_plane_len(int n) { return ((n + 63) / 64) * 64 + 32; }
@@ -200,7 +207,7 @@ __host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, in
     const int npad = ((n + 7) / 8) * 8 + 8;
     ResidLds l;
     int o = 0;
-    l.xs = o;   o = up(o + xbytes * (resid_hp(lmax) + npad));
+    l.xs = o;   o = up(o + xbytes * (resid_hp(lmax) + resid_xpad(n)));
     /* the MFMA planes are dead after the candidate sums; the residual-side regions reuse them */
     l.pl = o;
     const int pl_end = up(o + (planes ? 2 * 2 * mfma_plane_len(n) : 0));

@@ -227,35 +227,30 @@ __device__ __forceinline__ void chunk_sums_32(const int32_t (&w)[HP + 8], int i0
 }
 
 /* ---------------------------------------------------------------------------------------
- * MFMA candidate sums (PATH_S16, L <= 12): one v_mfma_f32_16x16x32_bf16 computes, for 16
+ * MFMA candidate sums (PATH_S16, L <= 12).  One v_mfma_f32_16x16x32_f16 computes, for 16
  * samples and 16 predictors (LPC orders 1..12, fixed orders 1..4),
- *     f = pred * 2^-sh - x[i] + (2^-(sh+1) - 1/2)         (C operand = the last term)
- * from bf16 planes of the sample bytes, x = 256*h + l (h signed, l unsigned), so that
- * floor(f + 1/2 - 2^-(sh+1)) = (pred >> sh) - x[i] = -r.  Every product and partial sum
- * is a multiple of 2^-(sh+1) below 2^24 in magnitude when (sum|c| + 2^sh) * 33023 < 2^22,
- * so the f32 accumulation is exact; the host-side bound check is per unit (phase A).
- * Then w = f + 1.5*2^23 rounds to the integer floor and its bit pattern is
- * 0x4B400000 + (-r): |r| is one v_sad_u32 accumulate.  Per sample and predictor: one
- * v_add_f32 and one v_sad_u32, against ceil((p+1)/2) dots + shift + sad on the VALU.
+ *     f = pred * 2^-sh - x[i] + (2^-(sh+1) - 1/2)          (the C operand is the last term)
+ * with every sample split exactly as x = 256*h + l (h signed, l unsigned byte, both exact
+ * in f16).  When (sum|c| + 2^sh) * 33023 < 2^22, every product and partial sum is a
+ * multiple of 2^-(sh+1) below 2^24 in magnitude, so the f32 accumulation is exact whatever
+ * its order; phase A checks that bound per unit (the VALU path takes the rest).  Then
+ * w = f + 1.5*2^23 rounds to floor(f) = (pred >> sh) - x[i] = -r, and the bit pattern of w
+ * is 0x4B400000 - r: |r| is one v_sad_u32 accumulate.  Per sample and predictor: one
+ * v_add_f32 and one v_sad_u32 (the VALU path: ceil((p+1)/2) dots + shift + sad).
  *
- * Block of 64 samples i0..i0+63, four MFMAs rho = 0..3: row s of MFMA rho is the sample
- * i0 + 4s + rho; its 16-wide tap window is positions [i0 + 4s - 12, i0 + 4s + 4) (the same
- * for every rho, so the A fragment is loaded once per block, 8-byte aligned), and B_rho
- * places each predictor's taps at window offset d + 12 + rho for x[i + d].
- * A fragment: lane l holds A[row l&15][k = 8(l>>4) + j]: k < 16 -> h plane, k >= 16 -> l
- * plane, window element k mod 16.  D: lane l holds column l&15, rows 4(l>>4) + r.
+ * Block of 64 samples i0..i0+63, MFMAs rho = 0..3: row s of MFMA rho is sample
+ * i0 + 4s + rho; its tap window is positions [e, e + 16), e = i0 + 4s - 12, the same for
+ * every rho, so the A fragment is built once per block; B_rho puts tap x[i + d] at window
+ * slot d + 12 + rho.  A fragment: lane l holds A[row l&15][k = 8(l>>4) + j]; k-block
+ * kb = l>>4 is window slots 4kb..4kb+3, j < 4 their h, j >= 4 their l, built from ONE
+ * 8-byte LDS read of the int16 samples.  D: lane l holds column l&15, rows 4(l>>4) + r.
  * ------------------------------------------------------------------------------------- */
-typedef short frag_ab __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float frag_cd __attribute__((ext_vector_type(4)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 constexpr uint32_t kFloorMagicBits = 0x4B400000u; /* 1.5 * 2^23 */
 constexpr float kFloorMagic = 12582912.0f;
 constexpr int kMfmaCoefLimit = 127; /* sum|c| + 2^sh; 127 * 33023 < 2^22 */
-
-__device__ __forceinline__ uint32_t bf16_hi(float v) { return __float_as_uint(v) & 0xffff0000u; }
-__device__ __forceinline__ uint32_t bf16_pack(float lo, float hi) {
-    return (__float_as_uint(lo) >> 16) | bf16_hi(hi);
-}
 
 /* v_sad_u32 acc + |a - b| as one instruction (the pattern match is lost on a constant b) */
 __device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t acc) {
@@ -263,16 +258,30 @@ __device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t acc
     return acc;
 }
 
-template <int LMAX, bool MASK>
-__device__ __forceinline__ uint32_t mfma_block(const uint16_t* pb, int i0, int eoff, const frag_ab (&B)[4],
+/* two int16 samples (lo, hi) -> f16 pairs of their high bytes (signed) and low bytes:
+ * 1024 + v is exact in f16 with the integer in the mantissa, so OR-ing the byte under
+ * 0x6400 and subtracting 1024 (1152 for the biased signed byte) converts exactly */
+__device__ __forceinline__ uint32_t f16_hi_bytes(uint32_t q) {
+    const uint32_t t = ((q >> 8) & 0x00FF00FFu) ^ 0x64806480u;
+    const half2v v = __builtin_bit_cast(half2v, t) - half2v{(_Float16)1152.0f, (_Float16)1152.0f};
+    return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ uint32_t f16_lo_bytes(uint32_t q) {
+    const uint32_t t = (q & 0x00FF00FFu) | 0x64006400u;
+    const half2v v = __builtin_bit_cast(half2v, t) - half2v{(_Float16)1024.0f, (_Float16)1024.0f};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+template <bool MASK>
+__device__ __forceinline__ uint32_t mfma_block(const int16_t* xs16, int i0, int eoff, const half8 (&B)[4],
                                                const frag_cd& C, int kb, int start, int n, uint32_t mb) {
-    const uint2 a0 = *reinterpret_cast<const uint2*>(pb + i0 + eoff);
-    const uint2 a1 = *reinterpret_cast<const uint2*>(pb + i0 + eoff + 4);
-    const uint4 av{a0.x, a0.y, a1.x, a1.y};
-    const bf16x8 A = __builtin_bit_cast(bf16x8, av);
+    const uint2 q = *reinterpret_cast<const uint2*>(xs16 + i0 + eoff);
+    const uint4 av{f16_hi_bytes(q.x), f16_hi_bytes(q.y), f16_lo_bytes(q.x), f16_lo_bytes(q.y)};
+    const half8 A = __builtin_bit_cast(half8, av);
     frag_cd D[4];
     static_for<4>([&](auto R_) {
-        D[R_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, B[R_]), C, 0, 0, 0);
+        constexpr int rho = R_;
+        D[rho] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[rho], C, 0, 0, 0);
     });
     uint32_t bs[4] = {0, 0, 0, 0};
     static_for<4>([&](auto R_) {
@@ -295,54 +304,70 @@ __device__ __forceinline__ uint32_t mfma_block(const uint16_t* pb, int i0, int e
 /* Sums for the fixed orders 1..4 and LPC orders 1..min(L,12) into red[wid][.] (the order-0
  * sum, sum|x|, comes from the staging pass). */
 template <int LMAX>
-__device__ __forceinline__ void mfma_candidate_sums(const uint16_t* Hp, const uint16_t* Lp, const int32_t* cfl,
-                                                    const int32_t* lsh, int L, int n, int lane, int wid, int nw,
+__device__ __forceinline__ void mfma_candidate_sums(const int16_t* xs16, const int32_t* cfl, const int32_t* lsh,
+                                                    int L, int n, int lane, int wid, int nw,
                                                     unsigned long long* red, uint32_t sumx) {
     using CT = CoefTables<LMAX>;
     constexpr int NSUM = 5 + LMAX;
     const int col = lane & 15, kb = lane >> 4;
     const bool lpc_col = col < 12;
-    int ncoef = 0, sh = 0, start = 0;
-    if (lpc_col) {
-        if (col + 1 <= L) {
-            sh = lsh[col];
-            start = lsh[LMAX + col];
-            ncoef = col + 1;
-        }
-    } else {
-        ncoef = col - 11;
-        start = ncoef;
+    /* this lane's predictor: coefficients cc[0..11] (zero past the order) and shift */
+    const bool lpc_live = lpc_col && col < L;
+    const int row = (col < LMAX ? col : LMAX - 1);
+    int cc[12];
+    {
+        const int4v* cr = reinterpret_cast<const int4v*>(cfl + row * CT::CPAD);
+        static_for<(CT::CPAD < 12 ? CT::CPAD : 12) / 4>([&](auto G_) {
+            constexpr int g = G_;
+            const int4v v = cr[g];
+            static_for<4>([&](auto E_) {
+                constexpr int e = E_;
+                cc[4 * g + e] = v[e];
+            });
+        });
+        static_for<12>([&](auto J_) {
+            constexpr int j = J_;
+            if constexpr (j >= CT::CPAD) cc[j] = 0;
+        });
+        const int k = col - 11; /* fixed order k: c_j = (-1)^j C(k, j+1) */
+        const int f0 = k, f1 = -(k * (k - 1) / 2), f2 = k * (k - 1) * (k - 2) / 6,
+                  f3 = -(k * (k - 1) * (k - 2) * (k - 3) / 24);
+        static_for<12>([&](auto J_) {
+            constexpr int j = J_;
+            const int fv = j == 0 ? f0 : j == 1 ? f1 : j == 2 ? f2 : j == 3 ? f3 : 0;
+            cc[j] = lpc_live ? cc[j] : (lpc_col ? 0 : fv);
+        });
     }
-    const float scale = (kb >> 1) ? 1.0f : 256.0f;
+    const int sh = lpc_live ? lsh[row] : 0;
+    const int start = lpc_col ? (lpc_live ? lsh[LMAX + row] : 0) : col - 11;
     const float inv = __uint_as_float((uint32_t)(127 - sh) << 23); /* 2^-sh */
-    frag_ab B[4];
+    /* tap value by jj = -1 - d: -1 for x[i] itself, c[jj] * 2^-sh for x[i-1-jj] */
+    auto tap = [&](int jj) -> float {
+        return jj == -1 ? -1.0f : (jj >= 0 && jj < 12) ? (float)cc[jj] * inv : 0.0f;
+    };
+    half8 B[4];
     static_for<4>([&](auto R_) {
         constexpr int rho = R_;
         static_for<8>([&](auto J_) {
             constexpr int j = J_;
-            const int d = 8 * (kb & 1) + j - 12 - rho; /* tap x[i + d] */
-            float v = 0.0f;
-            if (d == 0) {
-                v = -scale;
-            } else if (d < 0 && -1 - d < ncoef) {
-                const int jj = -1 - d;
-                const int c = lpc_col ? cfl[col * CT::CPAD + jj] : c_fixed_coef[col - 11][jj];
-                v = scale * (float)c * inv;
-            }
-            B[rho][j] = (short)(__float_as_uint(v) >> 16);
+            constexpr int jw = j & 3;                    /* window slot within the k-block */
+            /* slot w = 4kb + jw, d = w - 12 - rho, jj = -1 - d = 11 + rho - w */
+            const float v0 = tap(11 + rho - jw), v1 = tap(7 + rho - jw), v2 = tap(3 + rho - jw),
+                        v3 = tap(-1 + rho - jw);
+            const float v = kb == 0 ? v0 : kb == 1 ? v1 : kb == 2 ? v2 : v3;
+            B[rho][j] = (_Float16)(j < 4 ? 256.0f * v : v);
         });
     });
     const float cinit = 0.5f * inv - 0.5f;
     const frag_cd C{cinit, cinit, cinit, cinit};
-    const uint16_t* pb = (kb >> 1) ? Lp : Hp;
-    const int eoff = 4 * (lane & 15) - 12 + 8 * (kb & 1);
+    const int eoff = 4 * (lane & 15) - 12 + 4 * kb;
     uint64_t acc = 0;
     const uint32_t mb = kFloorMagicBits;
     const int nblk = (n + 63) >> 6;
     for (int blk = wid; blk < nblk; blk += nw) {
         const int i0 = blk << 6;
-        if (blk == 0 || i0 + 64 > n) acc += mfma_block<LMAX, true>(pb, i0, eoff, B, C, kb, start, n, mb);
-        else acc += mfma_block<LMAX, false>(pb, i0, eoff, B, C, kb, start, n, mb);
+        if (blk == 0 || i0 + 64 > n) acc += mfma_block<true>(xs16, i0, eoff, B, C, kb, start, n, mb);
+        else acc += mfma_block<false>(xs16, i0, eoff, B, C, kb, start, n, mb);
     }
     acc += (uint64_t)__shfl_xor((unsigned long long)acc, 16);
     acc += (uint64_t)__shfl_xor((unsigned long long)acc, 32);
@@ -505,9 +530,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         if (n % (1 << o) == 0) rmax_eff = o;
     const bool regz = resid_regz(n, rmax_eff, !WIDE && sizeof(ResT) == 4);
     const ResidLds lay = resid_lds_layout(LMAX, n, nw, 1 << (rmax_eff < 0 ? 0 : rmax_eff), S16 ? 2 : 4,
-                                          (int)sizeof(ResT), CT::BYTES, regz, MF);
-    uint16_t* Hp = reinterpret_cast<uint16_t*>(smem + lay.pl) + 16; /* bf16 high bytes [-16, plen-16) */
-    uint16_t* Lp = Hp + mfma_plane_len(n);                            /* bf16 low bytes */
+                                          (int)sizeof(ResT), CT::BYTES, regz, false);
     int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
     int32_t* xs32 = reinterpret_cast<int32_t*>(smem + lay.xs) + HP; /* [-HP, npad) (others) */
     ResT* zz = reinterpret_cast<ResT*>(smem + lay.zz);              /* [npad] (LDS-resident mode) */
@@ -537,35 +560,24 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     }
     if constexpr (S16) {
         for (int i = tid; i < HP; i += NT) xs16[i - HP] = 0;
-        for (int i = n + tid; i < npad; i += NT) xs16[i] = 0;
+        for (int i = n + tid; i < resid_xpad(n); i += NT) xs16[i] = 0;
         const int16_t* __restrict__ src = (const int16_t*)a.samples + u * a.stride;
         const int nv = n >> 3;
         if constexpr (MF) {
-            /* also the bf16 planes x = 256*h + l (h = x >> 8 signed, l = x & 255) and sum|x| */
-            const int plen = mfma_plane_len(n);
-            for (int i = tid; i < 16; i += NT) Hp[i - 16] = Lp[i - 16] = 0;
-            for (int i = n + tid; i < plen - 16; i += NT) Hp[i] = Lp[i] = 0;
+            /* also sum|x|: the fixed order-0 sum of the MFMA path */
             for (int v = tid; v < nv; v += NT) {
                 const uint4 q = *reinterpret_cast<const uint4*>(src + 8 * v);
                 *reinterpret_cast<uint4*>(xs16 + 8 * v) = q;
                 const uint32_t qd[4] = {q.x, q.y, q.z, q.w};
-                uint32_t hw[4], lw[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const uint32_t d = qd[e];
-                    const int32_t x0 = (int32_t)(d << 16) >> 16, x1 = (int32_t)d >> 16;
-                    hw[e] = bf16_pack((float)((int32_t)(d << 16) >> 24), (float)((int32_t)d >> 24));
-                    lw[e] = bf16_pack((float)(d & 0xffu), (float)((d >> 16) & 0xffu));
+                    const int32_t x0 = (int32_t)(qd[e] << 16) >> 16, x1 = (int32_t)qd[e] >> 16;
                     sumx += (uint32_t)(x0 < 0 ? -x0 : x0) + (uint32_t)(x1 < 0 ? -x1 : x1);
                 }
-                *reinterpret_cast<uint4*>(Hp + 8 * v) = uint4{hw[0], hw[1], hw[2], hw[3]};
-                *reinterpret_cast<uint4*>(Lp + 8 * v) = uint4{lw[0], lw[1], lw[2], lw[3]};
             }
             for (int i = nv * 8 + tid; i < n; i += NT) {
                 const int32_t x = src[i];
                 xs16[i] = (int16_t)x;
-                Hp[i] = (uint16_t)(__float_as_uint((float)(x >> 8)) >> 16);
-                Lp[i] = (uint16_t)(__float_as_uint((float)(x & 0xff)) >> 16);
                 sumx += (uint32_t)(x < 0 ? -x : x);
             }
         } else {
@@ -575,7 +587,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         }
     } else {
         for (int i = tid; i < HP; i += NT) xs32[i - HP] = 0;
-        for (int i = n + tid; i < npad; i += NT) xs32[i] = 0;
+        for (int i = n + tid; i < resid_xpad(n); i += NT) xs32[i] = 0;
         if (a.sample_bytes == 2) {
             const int16_t* __restrict__ src = (const int16_t*)a.samples + u * a.stride;
             const int nv = n >> 3;
@@ -638,7 +650,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
 
     /* ---- phase B: sum|r| for fixed orders 0..4 and LPC orders 1..L ---- */
     if (use_mfma) {
-        if constexpr (MF) mfma_candidate_sums<LMAX>(Hp, Lp, cfl, lsh, L, n, lane, wid, nw, red, sumx);
+        if constexpr (MF) mfma_candidate_sums<LMAX>(xs16, cfl, lsh, L, n, lane, wid, nw, red, sumx);
         if (a.stop_after == 2) return;
     } else {
     A acc[NSUM];
@@ -1113,7 +1125,7 @@ static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     const bool regz = resid_regz(a.n, rmax_eff, PATH != PATH_W64 && sizeof(ResT) == 4);
     const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff),
                                         PATH == PATH_S16 ? 2 : 4, (int)sizeof(ResT), CoefTables<LMAX>::BYTES,
-                                        regz, PATH == PATH_S16 && (LMAX == 8 || LMAX == 12)).total;
+                                        regz, false).total;
     auto kern = k_resid<LMAX, PATH, ResT>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
