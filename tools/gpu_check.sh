@@ -1,12 +1,13 @@
-# Quick GPU cycle: parity tests, then the default bench (c2), then optional extra args.
+# One GPU call: -m gpu tests, the default bench line, and the rocprofv3 evidence for it.
+# Usage (from this container): gpurun --timeout 1200 -- 'bash tools/gpu_check.sh <tag>'
 set -o pipefail
+TAG=${1:-r01}
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-tail -4 gpurun_out/pytest_gpu.log
-[ $rc -eq 0 ] || { grep -E "Error|assert" gpurun_out/pytest_gpu.log | head -20; exit 1; }
-timeout -k 10 600 python bench.py --cpu-seconds 2 "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
-python -c "
-import json; d=json.load(open('gpurun_out/bench.json'))
-print('value %.4g samples/s  ms/step %.2f' % (d['value'], d['ms_per_step']))
-print('kernels', {k: round(v,3) for k,v in d['kernels'].items()})
-print('roofline', d['roofline']['kernel'], round(d['roofline']['frac'],4), 'parity', d['parity'])"
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail -20 gpurun_out/smoke.log; exit 1; }
+cat gpurun_out/smoke.log
+timeout -k 10 400 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+bash tools/profile.sh $TAG
