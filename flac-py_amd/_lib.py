@@ -23,6 +23,13 @@ def load() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise FlacmiError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; "
                               f"g.build()'` (or make -C flac-py_amd/csrc)")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7 and binds
+        # device buffers/streams to it.  Loading torch first makes libflacmi.so resolve the
+        # same soname to that runtime; loaded the other way round torch finds no device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = C.CDLL(LIB_PATH)
         for name, (res, args) in abi.SIGNATURES.items():
             fn = getattr(lib, name)

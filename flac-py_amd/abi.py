@@ -25,6 +25,7 @@ STATUS_ASSERTION = 2
 STATUS_VALUE_ERROR = 3
 STATUS_OVERFLOW = 4
 STATUS_RESIDUAL_WIDE = 16
+STATUS_FRAME_TOO_LARGE = 17
 
 STATUS_EXCEPTION = {
     STATUS_ZERO_DIVISION: ZeroDivisionError,
@@ -50,6 +51,9 @@ SITE_NAMES = {
     12: "find_rice_parameter: math domain error (encoder.py:753)",
     13: "rice_size: negative shift count (encoder.py:758)",
     14: "residual does not fit the requested element width",
+    15: "coded_number.encode: frame number needs more than 31 bits (coded_number.py:38)",
+    16: "_put_subframe_lpc: assert precision - 1 != 0b1111 (encoder.py:619)",
+    17: "frame of 2^28 bytes or more (not packed by this build)",
 }
 
 MODE_REFERENCE = 0
@@ -135,6 +139,17 @@ class Outputs(C.Structure):
     ]
 
 
+class FrameParams(C.Structure):
+    _fields_ = [
+        ("channels", C.c_int32),
+        ("sample_size", C.c_int32),
+        ("qlp_precision", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("first_frame", C.c_int64),
+        ("reserved", C.c_int64 * 2),
+    ]
+
+
 # Every symbol include/flacmi.h declares, with its ctypes signature.
 SIGNATURES = {
     "flacmi_abi_version": (C.c_int, []),
@@ -146,6 +161,14 @@ SIGNATURES = {
                                         C.POINTER(Outputs), C.c_void_p]),
     "flacmi_analyze_host": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Params),
                                       C.POINTER(Outputs)]),
+    "flacmi_frame_sizes_device": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(FrameParams), C.c_void_p,
+                                            C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "flacmi_pack_frames_device": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(FrameParams), C.c_void_p,
+                                            C.c_void_p, C.c_int64, C.c_void_p, C.c_int32, C.c_int64, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p]),
+    "flacmi_encode_host": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Params), C.POINTER(FrameParams),
+                                     C.c_void_p, C.c_void_p]),
+    "flacmi_encode_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
     "flacmi_stream_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
                                       C.c_int64, C.c_void_p, C.c_void_p]),
     "flacmi_synth_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,

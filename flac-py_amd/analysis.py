@@ -26,6 +26,29 @@ def make_params(max_lpc_order: int, qlp_precision: int, rice_min: int, rice_max:
     return p
 
 
+def frame_params(channels: int, sample_size: int, qlp_precision: int, first_frame: int = 0) -> abi.FrameParams:
+    fp = abi.FrameParams()
+    fp.channels = channels
+    fp.sample_size = sample_size
+    fp.qlp_precision = qlp_precision
+    fp.first_frame = first_frame
+    return fp
+
+
+def device_batch(samples_ptr: int, sample_bytes: int, sample_bits: int, unit_stride: int, n_units: int,
+                 block_len: int, tail_len: int = 0, n_tail_units: int = 0) -> abi.Batch:
+    b = abi.Batch()
+    b.samples = samples_ptr
+    b.sample_bytes = sample_bytes
+    b.sample_bits = sample_bits
+    b.unit_stride = unit_stride
+    b.n_units = n_units
+    b.block_len = block_len
+    b.tail_len = tail_len
+    b.n_tail_units = n_tail_units
+    return b
+
+
 def params_stride_for(rice_max: int) -> int:
     return (1 << max(rice_max, 0)) + 1
 
@@ -123,6 +146,55 @@ class Analyzer:
         o.residual_stride = residual_stride
         check(self.lib.flacmi_analyze_device(self.ctx, C.byref(b), C.byref(params), C.byref(o), stream),
               "flacmi_analyze_device")
+
+    # ------------------------------------------------------------------------------
+    # frame writer (include/flacmi.h flacmi_frame_sizes_device / flacmi_pack_frames_device)
+    # ------------------------------------------------------------------------------
+    def encode_frames(self, samples: np.ndarray, params: abi.Params, block_len: int, tail_len: int = 0,
+                      n_tail_units: int = 0, sample_bits: int = 16, channels: int = 1,
+                      sample_size: int = 16, first_frame: int = 0):
+        """Host rows in -> (frame bytes, frame offsets [n_frames + 1], frame status [n_frames]).
+
+        Row f*channels + c is channel c of frame f.  A frame whose status is non-zero
+        (the reference's exception, (site << 16) | status) has no bytes."""
+        s = np.ascontiguousarray(samples)
+        if s.dtype not in (np.int16, np.int32) or s.ndim != 2:
+            raise ValueError("samples must be a 2-D int16 or int32 array")
+        n_units, stride = s.shape
+        b = abi.Batch()
+        b.samples = s.ctypes.data
+        b.sample_bytes = s.dtype.itemsize
+        b.sample_bits = sample_bits
+        b.unit_stride = stride
+        b.n_units = n_units
+        b.block_len = block_len
+        b.tail_len = tail_len
+        b.n_tail_units = n_tail_units
+        fp = frame_params(channels, sample_size, params.qlp_precision, first_frame)
+        n_frames = n_units // channels if channels else 0
+        offsets = np.zeros(n_frames + 1, dtype=np.int64)
+        status = np.zeros(max(n_frames, 1), dtype=np.int32)
+        check(self.lib.flacmi_encode_host(self.ctx, C.byref(b), C.byref(params), C.byref(fp),
+                                          offsets.ctypes.data, status.ctypes.data), "flacmi_encode_host")
+        total = int(offsets[-1])
+        out = np.empty(total, dtype=np.uint8)
+        check(self.lib.flacmi_encode_fetch(self.ctx, out.ctypes.data, total), "flacmi_encode_fetch")
+        return out, offsets, status[:n_frames]
+
+    def frame_sizes_device(self, batch: abi.Batch, fp: abi.FrameParams, meta_ptr: int, params_ptr: int,
+                           params_stride: int, offsets_ptr: int, status_ptr: int, stream: int = 0) -> None:
+        check(self.lib.flacmi_frame_sizes_device(self.ctx, C.byref(batch), C.byref(fp), meta_ptr, params_ptr,
+                                                 params_stride, offsets_ptr, status_ptr, stream),
+              "flacmi_frame_sizes_device")
+
+    def pack_frames_device(self, batch: abi.Batch, fp: abi.FrameParams, meta_ptr: int, params_ptr: int,
+                           params_stride: int, residual_ptr: int, residual_bytes: int, residual_stride: int,
+                           offsets_ptr: int, status_ptr: int, out_ptr: int, capacity: int,
+                           stream: int = 0) -> None:
+        check(self.lib.flacmi_pack_frames_device(self.ctx, C.byref(batch), C.byref(fp), meta_ptr, params_ptr,
+                                                 params_stride, residual_ptr, residual_bytes, residual_stride,
+                                                 offsets_ptr, status_ptr, out_ptr, capacity, stream),
+              "flacmi_pack_frames_device")
 
     def timing(self) -> dict:
         """Average k_lpc / k_resid / whole-call milliseconds over the analyze calls since

@@ -1,13 +1,11 @@
 """MSB-first bit writer/reader with the interface of flac/binary.py (mask :6-17,
 extract :20-30, Get :78-141, Put :144-216).
 
-Put accumulates bits in a Python integer and flushes whole bytes, and can append a
-pre-packed bit string (`bits`) in one step — the Rice codes of a residual are packed
-with numpy (`rice_bits`) instead of one `uint` call per bit.
+Put accumulates bits in a Python integer and flushes whole bytes.  It writes only the
+stream header here: frames (Rice codes, headers, CRCs) are written on the device
+(csrc/k_frame.hip).
 """
 from io import BytesIO
-
-import numpy as np
 
 
 def mask(n: int) -> int:
@@ -63,41 +61,10 @@ class Put(_Bits):
         assert self._bit_offset == 0
         self._out += bs
 
-    def bits(self, packed: bytes, nbits: int):
-        """Append the first nbits of an MSB-first packed bit string."""
-        if nbits <= 0:
-            return
-        if self._bit_offset == 0 and nbits % 8 == 0:
-            self._out += packed[: nbits // 8]
-            return
-        v = int.from_bytes(packed, "big") >> (8 * len(packed) - nbits)
-        self.uint(v, nbits)
-
     @property
     def buffer(self) -> bytes:
         assert self.is_aligned is True
         return bytes(self._out)
-
-
-def rice_bits(values: np.ndarray, params: np.ndarray) -> tuple:
-    """Rice codes of zig-zag values (encoder.py:798-806 per value: x >> p zeros, a one, the
-    low p bits MSB first) for per-value parameters, as (packed bytes, bit count)."""
-    x = np.asarray(values, dtype=np.uint64)
-    p = np.asarray(params, dtype=np.int64)
-    q = (x >> p.astype(np.uint64)).astype(np.int64)
-    width = q + 1 + p
-    ends = np.cumsum(width)
-    total = int(ends[-1]) if len(ends) else 0
-    starts = ends - width
-    bitmap = np.zeros(total, dtype=np.uint8)
-    one = starts + q
-    bitmap[one] = 1
-    pmax = int(p.max()) if len(p) else 0
-    for b in range(pmax):  # data bit b (from the MSB side) of every value with p > b
-        sel = p > b
-        shift = (p[sel] - 1 - b).astype(np.uint64)
-        bitmap[one[sel] + 1 + b] = ((x[sel] >> shift) & np.uint64(1)).astype(np.uint8)
-    return np.packbits(bitmap).tobytes(), total
 
 
 class Get(_Bits):

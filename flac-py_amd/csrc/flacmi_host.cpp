@@ -93,6 +93,40 @@ static void build_tables() {
 
 static void ensure_tables() { std::call_once(g_tables_once, build_tables); }
 
+/* CRC-16 tables of the frame writer (poly x^16 + x^15 + x^2 + 1, MSB first, init 0;
+ * crc.py:25-31): [4][256] slice-by-4 tables T_k[v] = v * x^(16+8k) mod P, then for
+ * b = 0..27 the linear map c -> c * x^(8*2^b) mod P as two 256-entry tables (low byte,
+ * high byte of c), built by repeated squaring of the map. */
+static std::vector<uint16_t> crc16_tables() {
+    std::vector<uint16_t> t(4 * 256 + 28 * 512);
+    auto mul8 = [&](uint32_t r) -> uint32_t { return ((r << 8) & 0xFFFF) ^ t[r >> 8]; };
+    for (uint32_t v = 0; v < 256; ++v) {
+        uint32_t r = v << 8;
+        for (int i = 0; i < 8; ++i) r = (r & 0x8000) ? ((r << 1) ^ 0x8005) & 0xFFFF : (r << 1) & 0xFFFF;
+        t[v] = (uint16_t)r;
+    }
+    for (int k = 1; k < 4; ++k)
+        for (uint32_t v = 0; v < 256; ++v) t[k * 256 + v] = (uint16_t)mul8(t[(k - 1) * 256 + v]);
+    uint32_t M[16], M2[16];
+    for (int i = 0; i < 16; ++i) M[i] = mul8(1u << i);
+    auto apply = [](const uint32_t* m, uint32_t c) {
+        uint32_t r = 0;
+        for (int i = 0; i < 16; ++i)
+            if (c >> i & 1) r ^= m[i];
+        return r;
+    };
+    for (int b = 0; b < 28; ++b) {
+        uint16_t* o = t.data() + 4 * 256 + b * 512;
+        for (uint32_t v = 0; v < 256; ++v) {
+            o[v] = (uint16_t)apply(M, v);
+            o[256 + v] = (uint16_t)apply(M, v << 8);
+        }
+        for (int i = 0; i < 16; ++i) M2[i] = apply(M, apply(M, 1u << i));
+        memcpy(M, M2, sizeof M);
+    }
+    return t;
+}
+
 /* Tukey(0.5) window exactly as encoder.py:423-440 computes it; padded with zeros. */
 static std::vector<double> tukey_window(int n, int pad) {
     std::vector<double> w((size_t)n + pad, 0.0);
@@ -122,6 +156,9 @@ struct flacmi_ctx {
     int32_t* d_sintab = nullptr;
     std::map<int, double*> windows;
     DevBuf rec, h_samples, h_meta, h_params, h_residual, h_acf, h_fs, h_ls, h_recs;
+    uint16_t* d_crc = nullptr;  /* CRC-16 slice tables [4][256] + power tables [28][512] */
+    DevBuf scan, h_offsets, h_status, h_frames;
+    int64_t frames_bytes = 0;   /* bytes of the last flacmi_encode_host call */
     static constexpr int kRing = 256;
     hipEvent_t ev[kRing][3] = {};
     int ncalls = 0; /* calls since the last timing reset */
@@ -189,6 +226,10 @@ flacmi_ctx* flacmi_create(int device) {
     if ((e = hipMalloc(&ctx->d_sintab, sizeof(int32_t) * 4096)) != hipSuccess) return bad(e, "hipMalloc");
     if ((e = hipMemcpy(ctx->d_sintab, g_sintab.data(), sizeof(int32_t) * 4096, hipMemcpyHostToDevice)) != hipSuccess)
         return bad(e, "hipMemcpy");
+    const std::vector<uint16_t> crc = crc16_tables();
+    if ((e = hipMalloc(&ctx->d_crc, sizeof(uint16_t) * crc.size())) != hipSuccess) return bad(e, "hipMalloc");
+    if ((e = hipMemcpy(ctx->d_crc, crc.data(), sizeof(uint16_t) * crc.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return bad(e, "hipMemcpy");
     return ctx;
 }
 
@@ -198,10 +239,12 @@ void flacmi_destroy(flacmi_ctx* ctx) {
     (void)hipDeviceSynchronize();
     for (auto& kv : ctx->windows) (void)hipFree(kv.second);
     for (DevBuf* b : {&ctx->rec, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
-                      &ctx->h_fs, &ctx->h_ls, &ctx->h_recs})
+                      &ctx->h_fs, &ctx->h_ls, &ctx->h_recs, &ctx->scan, &ctx->h_offsets, &ctx->h_status,
+                      &ctx->h_frames})
         if (b->p) (void)hipFree(b->p);
     if (ctx->d_log2thr) (void)hipFree(ctx->d_log2thr);
     if (ctx->d_sintab) (void)hipFree(ctx->d_sintab);
+    if (ctx->d_crc) (void)hipFree(ctx->d_crc);
     for (auto& slot : ctx->ev)
         for (auto& ev : slot)
             if (ev) (void)hipEventDestroy(ev);
@@ -464,6 +507,181 @@ int flacmi_analyze_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return 0;
 }
+
+}  // extern "C"
+
+/* ---- frame writer ---------------------------------------------------------------- */
+static int validate_frames(const flacmi_batch* b, const flacmi_frame_params* fp, int64_t* n_frames) {
+    if (!b || !fp) return fail(FLACMI_E_INVALID, "null argument");
+    if (fp->channels < 1 || fp->channels > 8) return fail(FLACMI_E_INVALID, "channels must be 1..8");
+    if (fp->sample_size < 1 || fp->sample_size > 32) return fail(FLACMI_E_INVALID, "sample_size must be 1..32");
+    if (fp->qlp_precision < 5 || fp->qlp_precision > 31) return fail(FLACMI_E_INVALID, "qlp_precision must be 5..31");
+    if (fp->first_frame < 0) return fail(FLACMI_E_INVALID, "first_frame must be >= 0");
+    if (b->n_units % fp->channels != 0) return fail(FLACMI_E_INVALID, "n_units must be a multiple of channels");
+    if (b->n_tail_units != 0 && b->n_tail_units != fp->channels)
+        return fail(FLACMI_E_INVALID, "the short last frame must hold exactly `channels` tail units");
+    if (b->block_len < 1 || b->block_len > FLACMI_MAX_BLOCK) return fail(FLACMI_E_INVALID, "block_len out of range");
+    *n_frames = b->n_units / fp->channels;
+    return 0;
+}
+
+static FrameArgs frame_args(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi_frame_params* fp,
+                            const flacmi_unit_meta* meta, const int32_t* rice_params, int64_t params_stride,
+                            int64_t n_frames) {
+    FrameArgs a{};
+    a.samples = b->samples;
+    a.stride = b->unit_stride;
+    a.sample_bytes = b->sample_bytes;
+    a.block_len = b->block_len;
+    a.tail_len = b->n_tail_units ? b->tail_len : b->block_len;
+    a.n_units = b->n_units;
+    a.n_tail_units = b->n_tail_units;
+    a.channels = fp->channels;
+    a.sample_size = fp->sample_size;
+    a.q = fp->qlp_precision;
+    a.first_frame = fp->first_frame;
+    a.n_frames = n_frames;
+    a.meta = meta;
+    a.rice_params = rice_params;
+    a.params_stride = params_stride;
+    a.crc_slice = ctx->d_crc;
+    a.crc_pow = ctx->d_crc + 4 * 256;
+    return a;
+}
+
+static int frame_sizes_impl(flacmi_ctx* ctx, FrameArgs& a, int64_t* offsets, int32_t* status, hipStream_t s) {
+    a.offsets = offsets;
+    a.status = status;
+    if (int rc = ensure_buf(ctx->scan, sizeof(int64_t) * (size_t)(frame_scan_blocks(a.n_frames) + 1))) return rc;
+    HIP_TRY(launch_frame_sizes(a, (int64_t*)ctx->scan.p, s));
+    return 0;
+}
+
+extern "C" {
+
+int flacmi_frame_sizes_device(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_frame_params* fp,
+                              const flacmi_unit_meta* meta, const int32_t* rice_params, int64_t params_stride,
+                              int64_t* frame_offsets, int32_t* frame_status, void* stream) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    int64_t nf = 0;
+    if (int rc = validate_frames(batch, fp, &nf)) return rc;
+    if (!meta || !rice_params || !frame_offsets || !frame_status) return fail(FLACMI_E_INVALID, "null buffer");
+    if (int rc = set_device(ctx)) return rc;
+    if (nf == 0) {
+        HIP_TRY(hipMemsetAsync(frame_offsets, 0, sizeof(int64_t), (hipStream_t)stream));
+        return 0;
+    }
+    FrameArgs a = frame_args(ctx, batch, fp, meta, rice_params, params_stride, nf);
+    return frame_sizes_impl(ctx, a, frame_offsets, frame_status, (hipStream_t)stream);
+}
+
+int flacmi_pack_frames_device(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_frame_params* fp,
+                              const flacmi_unit_meta* meta, const int32_t* rice_params, int64_t params_stride,
+                              const void* residual, int32_t residual_bytes, int64_t residual_stride,
+                              const int64_t* frame_offsets, int32_t* frame_status, uint8_t* out,
+                              int64_t out_capacity, void* stream) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    int64_t nf = 0;
+    if (int rc = validate_frames(batch, fp, &nf)) return rc;
+    if (!meta || !rice_params || !residual || !frame_offsets || !frame_status || (!out && out_capacity > 0))
+        return fail(FLACMI_E_INVALID, "null buffer");
+    if (residual_bytes != 4 && residual_bytes != 8) return fail(FLACMI_E_INVALID, "residual_bytes must be 4 or 8");
+    if (residual_stride < batch->block_len) return fail(FLACMI_E_INVALID, "residual_stride < block_len");
+    if (((uintptr_t)out & 3) != 0) return fail(FLACMI_E_INVALID, "out must be 4-byte aligned");
+    if (nf == 0) return 0;
+    if (int rc = set_device(ctx)) return rc;
+    FrameArgs a = frame_args(ctx, batch, fp, meta, rice_params, params_stride, nf);
+    a.residual = residual;
+    a.residual_bytes = residual_bytes;
+    a.residual_stride = residual_stride;
+    a.offsets = const_cast<int64_t*>(frame_offsets);
+    a.status = frame_status;
+    a.out = out;
+    a.capacity = out_capacity;
+    HIP_TRY(launch_pack(a, (hipStream_t)stream));
+    return 0;
+}
+
+int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_params* params,
+                       const flacmi_frame_params* fp, int64_t* frame_offsets, int32_t* frame_status) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    int64_t nf = 0;
+    if (int rc = validate_frames(batch, fp, &nf)) return rc;
+    if (!params || !frame_offsets || !frame_status) return fail(FLACMI_E_INVALID, "null argument");
+    ctx->frames_bytes = 0;
+    if (nf == 0) {
+        frame_offsets[0] = 0;
+        return 0;
+    }
+    if (int rc = set_device(ctx)) return rc;
+    const size_t nu = (size_t)batch->n_units;
+    const int64_t sstride = ((batch->block_len * batch->sample_bytes + 15) / 16) * 16 / batch->sample_bytes;
+    const int64_t pstride = (1LL << (params->rice_max > 0 ? params->rice_max : 0)) + 1;
+    if (int rc = ensure_buf(ctx->h_samples, nu * sstride * batch->sample_bytes)) return rc;
+    if (int rc = ensure_buf(ctx->h_meta, nu * sizeof(flacmi_unit_meta))) return rc;
+    if (int rc = ensure_buf(ctx->h_params, nu * pstride * sizeof(int32_t))) return rc;
+    if (int rc = ensure_buf(ctx->h_offsets, sizeof(int64_t) * (size_t)(nf + 1))) return rc;
+    if (int rc = ensure_buf(ctx->h_status, sizeof(int32_t) * (size_t)nf)) return rc;
+    flacmi_batch db = *batch;
+    db.samples = ctx->h_samples.p;
+    db.unit_stride = sstride;
+    HIP_TRY(hipMemcpy2DAsync(ctx->h_samples.p, sstride * batch->sample_bytes, batch->samples,
+                             batch->unit_stride * batch->sample_bytes, batch->block_len * batch->sample_bytes, nu,
+                             hipMemcpyHostToDevice, ctx->stream));
+    for (int rbytes = 4;; rbytes = 8) {
+        const int64_t rstride = ((batch->block_len * rbytes + 15) / 16) * 16 / rbytes;
+        if (int rc = ensure_buf(ctx->h_residual, nu * rstride * rbytes)) return rc;
+        flacmi_outputs o{};
+        o.meta = (flacmi_unit_meta*)ctx->h_meta.p;
+        o.rice_params = (int32_t*)ctx->h_params.p;
+        o.params_stride = pstride;
+        o.residual = ctx->h_residual.p;
+        o.residual_bytes = rbytes;
+        o.residual_stride = rstride;
+        if (int rc = validate(&db, params, &o)) return rc;
+        if (int rc = analyze_device_impl(ctx, &db, params, &o, ctx->stream)) return rc;
+        FrameArgs a = frame_args(ctx, &db, fp, o.meta, o.rice_params, pstride, nf);
+        if (int rc = frame_sizes_impl(ctx, a, (int64_t*)ctx->h_offsets.p, (int32_t*)ctx->h_status.p, ctx->stream))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(frame_offsets, ctx->h_offsets.p, sizeof(int64_t) * (nf + 1), hipMemcpyDeviceToHost,
+                               ctx->stream));
+        HIP_TRY(hipMemcpyAsync(frame_status, ctx->h_status.p, sizeof(int32_t) * nf, hipMemcpyDeviceToHost,
+                               ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        bool wide = false;
+        for (int64_t f = 0; f < nf && rbytes == 4; ++f)
+            if ((frame_status[f] & 0xffff) == FLACMI_STATUS_RESIDUAL_WIDE) wide = true;
+        if (wide) continue; /* a chosen residual needs 64 bits: redo with 8-byte rows */
+        const int64_t total = frame_offsets[nf];
+        if (int rc = ensure_buf(ctx->h_frames, (size_t)total + 16)) return rc;
+        a.residual = ctx->h_residual.p;
+        a.residual_bytes = rbytes;
+        a.residual_stride = rstride;
+        a.offsets = (int64_t*)ctx->h_offsets.p;
+        a.status = (int32_t*)ctx->h_status.p;
+        a.out = (uint8_t*)ctx->h_frames.p;
+        a.capacity = total;
+        HIP_TRY(launch_pack(a, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        ctx->frames_bytes = total;
+        return 0;
+    }
+}
+
+int flacmi_encode_fetch(flacmi_ctx* ctx, uint8_t* out, int64_t bytes) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    if (bytes < 0 || bytes > ctx->frames_bytes) return fail(FLACMI_E_INVALID, "at most %lld bytes are held",
+                                                            (long long)ctx->frames_bytes);
+    if (bytes == 0) return 0;
+    if (!out) return fail(FLACMI_E_INVALID, "null output");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipMemcpy(out, ctx->h_frames.p, (size_t)bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 int flacmi_stream_stats(flacmi_ctx* ctx, const flacmi_unit_meta* d_meta, int64_t n_units, int32_t block_len,
                         int32_t tail_len, int64_t n_tail_units, int64_t* d_stats, void* stream) {

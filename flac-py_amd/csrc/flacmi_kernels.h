@@ -48,6 +48,29 @@ struct ResidArgs {
     int32_t mfma;            /* 1 = MFMA candidate sums where exact (env FLACMI_NO_MFMA=1 -> 0) */
 };
 
+/* Frame writer (k_frame.hip): frame f = units [f*channels, (f+1)*channels). */
+struct FrameArgs {
+    const void* samples;     /* warm-up samples come from the batch rows */
+    int64_t stride;
+    int32_t sample_bytes;
+    int32_t block_len, tail_len;
+    int64_t n_units, n_tail_units;
+    int32_t channels, sample_size, q;
+    int64_t first_frame, n_frames;
+    const flacmi_unit_meta* meta;
+    const int32_t* rice_params;
+    int64_t params_stride;
+    const void* residual;
+    int32_t residual_bytes;
+    int64_t residual_stride;
+    int64_t* offsets;        /* [n_frames + 1] */
+    int32_t* status;         /* [n_frames] */
+    uint8_t* out;
+    int64_t capacity;
+    const uint16_t* crc_slice; /* [4][256] CRC-16 slice-by-4 tables */
+    const uint16_t* crc_pow;   /* [28][512] multiply-by-x^(8*2^b) tables */
+};
+
 struct ResidLaunch {
     int threads;             /* workgroup size (multiple of 64) */
     size_t lds_bytes;        /* dynamic LDS */
@@ -68,6 +91,11 @@ hipError_t launch_synth(void* dst, int32_t sample_bytes, int32_t bits, int64_t s
                         const int32_t* sintab, hipStream_t s);
 hipError_t launch_stats(const flacmi_unit_meta* meta, int64_t n_units, int32_t block_len,
                         int32_t tail_len, int64_t n_tail_units, int64_t* stats, hipStream_t s);
+
+/* frame sizes + exclusive scan into a.offsets; bsum: frame_scan_blocks(n_frames) words */
+hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s);
+int64_t frame_scan_blocks(int64_t n_frames);
+hipError_t launch_pack(const FrameArgs& a, hipStream_t s);
 
 hipError_t launch_selftest(int32_t which, const double* x, double* out, int32_t* status, int64_t n,
                            const double* log2thr, hipStream_t s);

@@ -1,0 +1,541 @@
+/* k_frame.hip — the FLAC frame writer on the device (residual bit
+ * packing and frame assembly).
+ *
+ * The reference writes every frame on the host one bit at a time through binary.Put:
+ *   frame header   encoder.py:194-234 (sync code, block-size / rate / channel / size codes,
+ *                  coded_number.py:7-39 frame number, CRC-8 crc.py:18-22)
+ *   subframes      encoder.py:553-627 (type byte, warm-up samples, LPC precision / shift /
+ *                  coefficients), put_residual :765-806 (coding method, partition order,
+ *                  per partition the parameter and the Rice codes: x >> p zeros, a one,
+ *                  the low p bits)
+ *   footer         encoder.py:159-163 (zero padding to a byte, CRC-16 crc.py:25-31)
+ *
+ * Here:
+ *   k_frame_sizes  one wave per frame: exact frame size from the analysis metadata
+ *                  (meta.rice_bits is the reference's size estimate, which counts 4 + 4|5
+ *                  header bits per partition; the written size differs from it by a
+ *                  closed form), the frame's status (first reference exception), then a
+ *                  three-kernel exclusive scan gives every frame its byte offset.
+ *   k_pack         one workgroup per frame.  Every field is OR-ed into an LDS window of
+ *                  kWinWords 32-bit words at its exact bit position (positions from a
+ *                  workgroup scan of per-value code lengths, 8 values per thread); a full
+ *                  window is flushed to HBM with coalesced dword stores (byte stores only
+ *                  on the frame's first and last word, which it shares with its
+ *                  neighbours).  The CRC-16 is computed on the fly: each thread folds its
+ *                  contiguous run of window words with slice-by-4 tables and moves the
+ *                  partial CRC to the frame's end with x^(8d) tables (the CRC is linear
+ *                  and starts from 0, so CRC(A||B) = CRC(A)*x^(8|B|) + CRC(B) mod P).
+ *
+ * Bit coordinates inside k_pack are "aligned": bit 0 is the MSB of the 32-bit word that
+ * holds the frame's first byte, so window word k is output word (F >> 2) + wb + k.  The
+ * window words hold bits MSB first; stores byte-swap them. */
+#include "device_common.h"
+
+namespace flacmi {
+
+constexpr int kWinWords = 4096;           /* 16 KB LDS window */
+constexpr int kPackThreads = 256;
+constexpr int kCrcPowLevels = 28;         /* frames < 2^28 bytes */
+
+/* block-size code (encoder.py:245-255, common.py:85-105): 0 = not encodable */
+__device__ __forceinline__ int bs_code(int bs) {
+    switch (bs) {
+        case 192: return 1;
+        case 576: return 2;
+        case 1152: return 3;
+        case 2304: return 4;
+        case 4608: return 5;
+        case 256: return 8;
+        case 512: return 9;
+        case 1024: return 10;
+        case 2048: return 11;
+        case 4096: return 12;
+        case 8192: return 13;
+        case 16384: return 14;
+        case 32768: return 15;
+        default: break;
+    }
+    const int bl = 32 - __builtin_clz((unsigned)bs);
+    return bl <= 8 ? 6 : bl <= 16 ? 7 : 0;
+}
+
+/* Frame header bytes (CRC-8 included) into h[16]; returns the byte count, or -1 when the
+ * frame number needs more than 31 bits (coded_number.py:36-38 ValueError). */
+__device__ int frame_header(int64_t fno, int bs, uint8_t* h) {
+    const int code = bs_code(bs);
+    h[0] = 0xFF;
+    h[1] = 0xF8;                /* sync 0b111111111111100 + BlockingStrategy.Fixed (0) */
+    h[2] = (uint8_t)(code << 4); /* sample rate: from STREAMINFO (0000) */
+    h[3] = 0x10;                /* channels L_R (0001, encoder.py:95), sample size from STREAMINFO, 0 */
+    const int bl = fno == 0 ? 0 : 64 - __builtin_clzll((unsigned long long)fno);
+    if (bl > 31) return -1;
+    const int size = bl <= 7 ? 1 : bl <= 11 ? 2 : bl <= 16 ? 3 : bl <= 21 ? 4 : bl <= 26 ? 5 : 6;
+    int k = 4;
+    if (size == 1) {
+        h[k++] = (uint8_t)fno;
+    } else {
+        h[k++] = (uint8_t)(((0xFFu << (8 - size)) & 0xFFu) | (uint32_t)((fno >> (6 * (size - 1))) & 0x3F));
+        for (int i = size - 2; i >= 0; --i) h[k++] = (uint8_t)(0x80 | ((fno >> (6 * i)) & 0x3F));
+    }
+    if (code == 6) h[k++] = (uint8_t)(bs - 1);
+    if (code == 7) {
+        h[k++] = (uint8_t)((bs - 1) >> 8);
+        h[k++] = (uint8_t)(bs - 1);
+    }
+    uint32_t c = 0; /* CRC-8, x^8 + x^2 + x + 1, init 0 (crc.py:18-22) */
+    for (int i = 0; i < k; ++i) {
+        c ^= h[i];
+        for (int b = 0; b < 8; ++b) c = (c & 0x80) ? ((c << 1) ^ 0x07) & 0xFF : (c << 1) & 0xFF;
+    }
+    h[k++] = (uint8_t)c;
+    return k;
+}
+
+__device__ __forceinline__ int unit_len(const FrameArgs& a, int64_t u) {
+    return u >= a.n_units - a.n_tail_units ? a.tail_len : a.block_len;
+}
+
+/* Bits of the subframe up to the first partition (encoder.py:553-627, :766-767). */
+__device__ __forceinline__ uint32_t sub_prefix_bits(const flacmi_unit_meta& m, int ss, int q) {
+    const bool lpc = m.kind == FLACMI_KIND_LPC;
+    return 8u + (uint32_t)m.order * (uint32_t)ss + (lpc ? 9u + (uint32_t)m.ncoefs * (uint32_t)q : 0u) + 6u;
+}
+
+/* Written residual bits (partition parameters + Rice codes) from the reference's estimate
+ * rice_bits = sum_k [4 + (p_k > 14 ? 5 : 4) + data_k] (encoder.py:714-727):
+ *   Rice4Bit: sum_k [4 + data_k]          = rice_bits - 4 n_parts
+ *   Rice5Bit: sum_k [5 + data_k]          = rice_bits - 3 n_parts - #{p_k > 14} */
+__device__ __forceinline__ int64_t sub_residual_bits(const flacmi_unit_meta& m, int cnt14) {
+    return m.coding_method == 5 ? m.rice_bits - 3LL * m.n_parts - cnt14 : m.rice_bits - 4LL * m.n_parts;
+}
+
+/* ====================================================================================
+ * k_frame_sizes: one wave per frame
+ * ==================================================================================== */
+__global__ __launch_bounds__(256) void k_frame_sizes(FrameArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (f >= a.n_frames) return;
+    const int64_t u0 = f * a.channels;
+    const int bs = unit_len(a, u0);
+    uint8_t h[16];
+    int st = 0;
+    const int hb = frame_header(a.first_frame + f, bs, h);
+    if (hb < 0) st = (FLACMI_SITE_CODED_NUMBER << 16) | FLACMI_STATUS_VALUE_ERROR;
+    int64_t bits = 0;
+    for (int c = 0; c < a.channels && st == 0; ++c) {
+        const flacmi_unit_meta& m = a.meta[u0 + c];
+        if (m.status != 0) {
+            st = (m.site << 16) | m.status;
+            break;
+        }
+        if (m.kind == FLACMI_KIND_LPC && ((a.q - 1) & 15) == 15) {
+            st = (FLACMI_SITE_LPC_PRECISION << 16) | FLACMI_STATUS_ASSERTION;
+            break;
+        }
+        int cnt = 0;
+        if (m.coding_method == 5) {
+            const int32_t* rp = a.rice_params + (u0 + c) * a.params_stride;
+            for (int k = lane; k < m.n_parts; k += 64) cnt += rp[k] > 14 ? 1 : 0;
+            for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+        }
+        bits += (int64_t)sub_prefix_bits(m, a.sample_size, a.q) + sub_residual_bits(m, cnt);
+    }
+    int64_t bytes = 0;
+    if (st == 0) {
+        bytes = hb + (bits + 7) / 8 + 2;
+        if (bytes >= (1LL << kCrcPowLevels)) {
+            st = (FLACMI_SITE_FRAME_SIZE << 16) | FLACMI_STATUS_FRAME_TOO_LARGE;
+            bytes = 0;
+        }
+    }
+    if (lane == 0) {
+        a.offsets[f + 1] = bytes;
+        a.status[f] = st;
+        if (f == 0) a.offsets[0] = 0;
+    }
+}
+
+/* ---- exclusive scan of frame sizes (in place on offsets[1..n]) ---------------------- */
+constexpr int kScanItems = 8;
+constexpr int kScanBlock = 256 * kScanItems;
+
+__device__ __forceinline__ int64_t block_incl_scan(int64_t v, int64_t* sh, int64_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) sh[wid] = v;
+    __syncthreads();
+    int64_t pre = 0, tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        if (w < wid) pre += sh[w];
+        tot += sh[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return v + pre;
+}
+
+__global__ __launch_bounds__(256) void k_scan_local(int64_t* x, int64_t n, int64_t* bsum) {
+    __shared__ int64_t sh[4];
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanItems;
+    int64_t v[kScanItems], s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = base + k < n ? x[base + k] : 0;
+        s += v[k];
+    }
+    int64_t tot;
+    const int64_t incl = block_incl_scan(s, sh, &tot);
+    int64_t run = incl - s;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        run += v[k];
+        if (base + k < n) x[base + k] = run;
+    }
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_scan_sums(int64_t* bsum, int64_t nb) {
+    __shared__ int64_t sh[4];
+    int64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += 256) {
+        const int64_t i = b0 + threadIdx.x;
+        const int64_t v = i < nb ? bsum[i] : 0;
+        int64_t tot;
+        const int64_t incl = block_incl_scan(v, sh, &tot);
+        if (i < nb) bsum[i] = carry + incl - v; /* exclusive */
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_scan_add(int64_t* x, int64_t n, const int64_t* bsum) {
+    const int64_t base = (int64_t)blockIdx.x * kScanBlock;
+    const int64_t add = bsum[blockIdx.x];
+    for (int k = threadIdx.x; k < kScanBlock; k += 256)
+        if (base + k < n) x[base + k] += add;
+}
+
+/* ====================================================================================
+ * k_pack
+ * ==================================================================================== */
+struct CrcTabs {
+    const uint16_t* slice; /* [4][256]: T_k[v] = v * x^(16+8k) mod P */
+    const uint16_t* pw;    /* [kCrcPowLevels][512]: c -> c * x^(8*2^b) mod P, low byte | high byte */
+};
+
+__device__ __forceinline__ uint32_t crc16_mulpow(uint32_t c, int64_t d, const uint16_t* __restrict__ pw) {
+    for (int b = 0; d != 0 && c != 0; ++b, d >>= 1)
+        if (d & 1) c = (uint32_t)pw[b * 512 + (c & 0xFF)] ^ (uint32_t)pw[b * 512 + 256 + (c >> 8)];
+    return c;
+}
+
+/* OR the w-bit value v (right-aligned, 1 <= w <= 64) at aligned bit position pos into the
+ * window covering aligned words [wb, wb + kWinWords); parts outside are skipped. */
+__device__ __forceinline__ void win_or(uint32_t* win, uint32_t wb, uint32_t pos, uint64_t v, int w) {
+    const uint32_t end = pos + (uint32_t)w;
+    uint32_t lo = pos > wb * 32u ? pos : wb * 32u;
+    const uint32_t wend_all = (wb + kWinWords) * 32u;
+    const uint32_t hi = end < wend_all ? end : wend_all;
+    while (lo < hi) {
+        const uint32_t word = lo >> 5;
+        const uint32_t we = (word + 1) * 32u;
+        const uint32_t pe = hi < we ? hi : we;
+        const int nb = (int)(pe - lo);
+        const uint32_t piece = (uint32_t)((v >> (end - pe)) & ((nb == 64 ? 0ull : (1ull << nb)) - 1ull));
+        atomicOr(&win[word - wb], piece << (32 - (int)(lo & 31) - nb));
+        lo = pe;
+    }
+}
+
+/* Flush window words [0, nw) (aligned words wb..wb+nw) to the output: CRC-16 contributions
+ * of the bytes in [F, E) first, then (final) the CRC itself at E, then the stores. */
+__device__ void win_flush(const FrameArgs& a, uint32_t* win, const uint16_t* ct, uint32_t wb, int nw, bool final,
+                          int64_t F, int64_t Fend, uint32_t& crc_acc, uint32_t* red) {
+    const int tid = threadIdx.x, NT = blockDim.x;
+    const int64_t E = Fend - 2;
+    const int64_t gw0 = (F >> 2) + wb; /* output word of window word 0 */
+    {
+        const int wpt = (nw + NT - 1) / NT;
+        const int k0 = tid * wpt, k1 = k0 + wpt < nw ? k0 + wpt : nw;
+        uint32_t c = 0;
+        int64_t R = -1;
+        for (int k = k0; k < k1; ++k) {
+            const int64_t gb = 4 * (gw0 + k);
+            const uint32_t w = win[k];
+            if (gb >= F && gb + 4 <= E) {
+                c = (uint32_t)ct[3 * 256 + ((c >> 8) ^ (w >> 24))] ^ (uint32_t)ct[2 * 256 + ((c ^ (w >> 16)) & 0xFF)] ^
+                    (uint32_t)ct[256 + ((w >> 8) & 0xFF)] ^ (uint32_t)ct[w & 0xFF];
+                R = gb + 4;
+            } else {
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t B = gb + j;
+                    if (B >= F && B < E) {
+                        c = ((c << 8) & 0xFFFF) ^ (uint32_t)ct[(c >> 8) ^ ((w >> (24 - 8 * j)) & 0xFF)];
+                        R = B + 1;
+                    }
+                }
+            }
+        }
+        if (R >= 0) crc_acc ^= crc16_mulpow(c, E - R, a.crc_pow);
+    }
+    __syncthreads(); /* every CRC read of the window precedes the stores below */
+    if (final) {
+        uint32_t v = crc_acc;
+        for (int o = 32; o >= 1; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o);
+        if ((tid & 63) == 0) red[tid >> 6] = v;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t crc = 0;
+            for (int w2 = 0; w2 < NT / 64; ++w2) crc ^= red[w2];
+            const uint32_t pos = (uint32_t)(8 * (F & 3) + 8 * (E - F));
+            win_or(win, wb, pos, crc & 0xFFFF, 16);
+        }
+        __syncthreads();
+    }
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out);
+    for (int k = tid; k < nw; k += NT) {
+        const int64_t g = gw0 + k;
+        const uint32_t w = win[k];
+        if (4 * g >= F && 4 * g + 4 <= Fend) {
+            out32[g] = __builtin_bswap32(w);
+        } else {
+            for (int j = 0; j < 4; ++j) {
+                const int64_t B = 4 * g + j;
+                if (B >= F && B < Fend) a.out[B] = (uint8_t)(w >> (24 - 8 * j));
+            }
+        }
+        win[k] = 0;
+    }
+    __syncthreads();
+}
+
+template <typename ZT>
+__global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
+    __shared__ uint32_t win[kWinWords];
+    __shared__ uint16_t ct[4 * 256];
+    __shared__ uint8_t hdr[16];
+    __shared__ uint32_t sub_start[9];
+    __shared__ int32_t cnt14[8];
+    __shared__ uint32_t red[8];
+    __shared__ int hb_s;
+    const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t f = blockIdx.x;
+    if (a.offsets[a.n_frames] > a.capacity) {
+        if (f == 0 && tid == 0) a.status[0] = (FLACMI_SITE_FRAME_SIZE << 16) | FLACMI_STATUS_FRAME_TOO_LARGE;
+        return;
+    }
+    if (a.status[f] != 0) return;
+    const int64_t F = a.offsets[f], Fend = a.offsets[f + 1];
+    const int64_t u0 = f * a.channels;
+    const int C = a.channels;
+    for (int i = tid; i < 4 * 256; i += NT) ct[i] = a.crc_slice[i];
+    for (int i = tid; i < kWinWords; i += NT) win[i] = 0;
+    if (tid < 8) cnt14[tid] = 0;
+    if (tid == 0) hb_s = frame_header(a.first_frame + f, unit_len(a, u0), hdr);
+    __syncthreads();
+    for (int c = 0; c < C; ++c) {
+        const flacmi_unit_meta& m = a.meta[u0 + c];
+        if (m.coding_method == 5) {
+            const int32_t* rp = a.rice_params + (u0 + c) * a.params_stride;
+            int cnt = 0;
+            for (int k = tid; k < m.n_parts; k += NT) cnt += rp[k] > 14 ? 1 : 0;
+            if (cnt) atomicAdd(&cnt14[c], cnt);
+        }
+    }
+    __syncthreads();
+    const int hb = hb_s;
+    const uint32_t A = (uint32_t)(8 * (F & 3)); /* aligned bit of the frame's first bit */
+    if (tid == 0) {
+        uint32_t s = A + 8u * (uint32_t)hb;
+        for (int c = 0; c < C; ++c) {
+            const flacmi_unit_meta& m = a.meta[u0 + c];
+            sub_start[c] = s;
+            s += sub_prefix_bits(m, a.sample_size, a.q) + (uint32_t)sub_residual_bits(m, cnt14[c]);
+        }
+        sub_start[C] = s;
+    }
+    __syncthreads();
+
+    uint32_t wb = 0, crc_acc = 0;
+    /* run `body` until the segment ending at aligned bit seg_end is in the window; full
+     * windows are flushed in between (uniform control flow) */
+    auto segment = [&](uint32_t seg_end, auto&& body) __attribute__((always_inline)) {
+        while (true) {
+            body();
+            if (seg_end <= (wb + kWinWords) * 32u) break;
+            __syncthreads();
+            win_flush(a, win, ct, wb, kWinWords, false, F, Fend, crc_acc, red);
+            wb += kWinWords;
+        }
+    };
+    /* frame header: byte fields */
+    segment(A + 8u * hb, [&]() {
+        if (tid < hb) win_or(win, wb, A + 8u * tid, hdr[tid], 8);
+    });
+    const int ss = a.sample_size, q = a.q;
+    for (int c = 0; c < C; ++c) {
+        const int64_t u = u0 + c;
+        const flacmi_unit_meta& m = a.meta[u];
+        const int n = unit_len(a, u);
+        const int order = m.order, ncoefs = m.ncoefs, method = m.coding_method;
+        const bool lpc = m.kind == FLACMI_KIND_LPC;
+        const uint32_t s0 = sub_start[c];
+        const uint32_t pre = sub_prefix_bits(m, ss, q);
+        /* subframe header, warm-up, LPC fields, residual header: field t per thread */
+        const int nfields = 1 + order + (lpc ? 2 + ncoefs : 0) + 2;
+        segment(s0 + pre, [&]() {
+            for (int t = tid; t < nfields; t += NT) {
+                uint32_t pos;
+                uint64_t v;
+                int w;
+                if (t == 0) {
+                    pos = s0;
+                    v = lpc ? (uint64_t)((0x20 | (order - 1)) << 1) : (uint64_t)((0x08 | order) << 1);
+                    w = 8;
+                } else if (t <= order) {
+                    const int j = t - 1;
+                    const int64_t x = a.sample_bytes == 2 ? (int64_t)((const int16_t*)a.samples)[u * a.stride + j]
+                                                          : (int64_t)((const int32_t*)a.samples)[u * a.stride + j];
+                    pos = s0 + 8 + (uint32_t)j * ss;
+                    v = (uint64_t)x & (ss == 64 ? ~0ull : ((1ull << ss) - 1));
+                    w = ss;
+                } else {
+                    const uint32_t b = s0 + 8 + (uint32_t)order * ss;
+                    const int t2 = t - 1 - order;
+                    if (lpc && t2 == 0) {
+                        pos = b;
+                        v = (uint64_t)((q - 1) & 15);
+                        w = 4;
+                    } else if (lpc && t2 == 1) {
+                        pos = b + 4;
+                        v = (uint64_t)(m.shift & 31);
+                        w = 5;
+                    } else if (lpc && t2 < 2 + ncoefs) {
+                        const int j = t2 - 2;
+                        pos = b + 9 + (uint32_t)j * q;
+                        v = (uint64_t)(int64_t)m.coefs[j] & ((1ull << q) - 1);
+                        w = q;
+                    } else {
+                        const int t3 = t2 - (lpc ? 2 + ncoefs : 0);
+                        const uint32_t b2 = b + (lpc ? 9u + (uint32_t)ncoefs * q : 0u);
+                        if (t3 == 0) {
+                            pos = b2;
+                            v = method == 5 ? 1 : 0;
+                            w = 2;
+                        } else {
+                            pos = b2 + 2;
+                            v = (uint64_t)(m.part_order & 15);
+                            w = 4;
+                        }
+                    }
+                }
+                win_or(win, wb, pos, v, w);
+            }
+        });
+        /* partitions: parameter + Rice codes, 8 residual values per thread per tile */
+        const int ps = n >> m.part_order;
+        const int32_t* __restrict__ rp = a.rice_params + u * a.params_stride;
+        const ZT* __restrict__ zrow = reinterpret_cast<const ZT*>(a.residual) + u * a.residual_stride;
+        const int nch = (n + 7) >> 3;
+        const uint64_t pmask_m = (1ull << method) - 1;
+        uint32_t tile_base = s0 + pre;
+        for (int c0 = 0; c0 < nch; c0 += NT) {
+            const int ch = c0 + tid;
+            const int i0 = 8 * ch;
+            ZT z[8];
+            int pp[8];
+            uint32_t len[8];
+            uint32_t tsum = 0;
+            int part = i0 / ps;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = i0 + k;
+                const bool valid = ch < nch && i >= order && i < n;
+                while ((part + 1) * ps <= i) ++part;
+                z[k] = valid ? zrow[i] : (ZT)0;
+                const int p = valid ? rp[part] : 0;
+                const bool first = valid && (i == order || (i == part * ps && i > order));
+                pp[k] = first ? p | 0x100 : p;
+                const uint32_t qv = p >= (int)(8 * sizeof(ZT)) ? 0u : (uint32_t)(z[k] >> p);
+                len[k] = valid ? (first ? (uint32_t)method : 0u) + qv + 1u + (uint32_t)p : 0u;
+                tsum += len[k];
+            }
+            /* workgroup exclusive scan of tsum */
+            uint32_t v = tsum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)v, o);
+                if (lane >= o) v += t;
+            }
+            if (lane == 63) red[wid] = v;
+            __syncthreads();
+            uint32_t pre_w = 0, tot = 0;
+            for (int w2 = 0; w2 < NT / 64; ++w2) {
+                const uint32_t s = red[w2];
+                if (w2 < wid) pre_w += s;
+                tot += s;
+            }
+            __syncthreads();
+            const uint32_t tstart = tile_base + pre_w + v - tsum;
+            segment(tile_base + tot, [&]() {
+                uint32_t pos = tstart;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (len[k] != 0) {
+                        const int p = pp[k] & 0xFF;
+                        uint32_t at = pos;
+                        if (pp[k] & 0x100) {
+                            win_or(win, wb, at, (uint64_t)p & pmask_m, method);
+                            at += (uint32_t)method;
+                        }
+                        const uint32_t qv = p >= (int)(8 * sizeof(ZT)) ? 0u : (uint32_t)(z[k] >> p);
+                        const uint64_t val = (1ull << p) | ((uint64_t)z[k] & ((1ull << p) - 1));
+                        win_or(win, wb, at + qv, val, p + 1);
+                        pos += len[k];
+                    }
+                }
+            });
+            tile_base += tot;
+        }
+    }
+    __syncthreads();
+    /* padding is already zero; the CRC-16 goes at byte E = Fend - 2 */
+    const uint32_t endbit = (uint32_t)(8 * (F & 3) + 8 * (Fend - F));
+    /* the CRC bytes must land in the final window */
+    while (endbit > (wb + kWinWords) * 32u) {
+        win_flush(a, win, ct, wb, kWinWords, false, F, Fend, crc_acc, red);
+        wb += kWinWords;
+    }
+    const int nw = (int)((endbit + 31) / 32 - wb);
+    win_flush(a, win, ct, wb, nw, true, F, Fend, crc_acc, red);
+}
+
+hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s) {
+    if (a.n_frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_frame_sizes, dim3((unsigned)((a.n_frames + 3) / 4)), dim3(256), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t n = a.n_frames;
+    const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    hipLaunchKernelGGL(k_scan_local, dim3((unsigned)nb), dim3(256), 0, s, a.offsets + 1, n, bsum);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, s, bsum, nb);
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(256), 0, s, a.offsets + 1, n, (const int64_t*)bsum);
+    return hipGetLastError();
+}
+
+int64_t frame_scan_blocks(int64_t n_frames) { return (n_frames + kScanBlock - 1) / kScanBlock; }
+
+hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
+    if (a.n_frames <= 0) return hipSuccess;
+    if (a.residual_bytes == 8)
+        hipLaunchKernelGGL(k_pack<uint64_t>, dim3((unsigned)a.n_frames), dim3(kPackThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_pack<uint32_t>, dim3((unsigned)a.n_frames), dim3(kPackThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace flacmi

@@ -518,7 +518,6 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     const int64_t u = a.unit0 + gid;
     const int n = a.n, L = a.L;
     const int nch = (n + 7) >> 3;
-    const int npad = nch * 8 + 8;
     /* LPC records exist in the reference and LPC-only modes */
     const bool ref_mode = a.mode == FLACMI_MODE_REFERENCE || a.mode == FLACMI_MODE_LPC_ONLY;
     const bool do_lpc = LMAX > 0 && ref_mode;

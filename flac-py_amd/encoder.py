@@ -17,15 +17,16 @@ import numpy as np
 
 from . import abi
 from . import coded_number
+from ._lib import FlacmiError
 from .analysis import Analyzer, make_params, params_stride_for
-from .binary import Put, rice_bits
+from .binary import Put
 from .common import (
-    CHANNELS_ENCODING, CRC8_POLYNOMIAL, CRC16_POLYNOMIAL, FRAME_SYNC_CODE, MAGIC,
+    CHANNELS_ENCODING, CRC8_POLYNOMIAL, FRAME_SYNC_CODE, MAGIC,
     BLOCK_SIZE_ENCODING, BlockingStrategy, Channels, FrameHeader, MetadataBlockHeader,
     MetadataBlockType, Residual, RiceCodingMethod, RicePartition, Streaminfo, SubframeFixed,
     SubframeHeader, SubframeLPC, SubframeTypeFixed, SubframeTypeLPC,
 )
-from .crc import crc8, crc16
+from .crc import crc8
 from .utils import batch
 
 __all__ = ["EncoderParameters", "encode", "encode_subframe_fixed", "encode_subframe_lpc",
@@ -73,15 +74,22 @@ _SITE_EXCEPTION = {
     11: (AssertionError, ""),
     12: (ValueError, "math domain error"),
     13: (ValueError, "negative shift count"),
+    15: (ValueError, "Cannot encode coded number"),
+    16: (AssertionError, ""),
 }
 
 
-def _raise_for(meta_row) -> None:
-    st, site = int(meta_row["status"]), int(meta_row["site"])
+def _raise_status(st: int, site: int) -> None:
     if st == abi.STATUS_OK:
         return
+    if st == abi.STATUS_FRAME_TOO_LARGE:
+        raise FlacmiError(abi.SITE_NAMES[17])
     exc, msg = _SITE_EXCEPTION.get(site, (abi.STATUS_EXCEPTION.get(st, RuntimeError), ""))
     raise exc(msg) if msg else exc()
+
+
+def _raise_for(meta_row) -> None:
+    _raise_status(int(meta_row["status"]), int(meta_row["site"]))
 
 
 def _rice_range(r: range):
@@ -166,59 +174,12 @@ def put_frame_header(header: FrameHeader) -> Put:
     return put
 
 
-def _put_residual(put: Put, zz: np.ndarray, params, n: int, order: int, part_order: int, method: int):
-    put.uint(0b00 if method == 4 else 0b01, 2)
-    put.uint(part_order, 4)
-    ps = n >> part_order
-    lens = [ps - order] + [ps] * ((1 << part_order) - 1)
-    pos = 0
-    for prm, ln in zip(params, lens):
-        put.uint(int(prm), method)
-        packed, nbits = rice_bits(zz[pos:pos + ln], np.full(ln, int(prm), dtype=np.int64))
-        put.bits(packed, nbits)
-        pos += ln
-
-
-def _put_subframe(put: Put, samples: np.ndarray, m, zz_row: np.ndarray, params_row, n: int,
-                  sample_size: int, precision: int):
-    order = int(m["order"])
-    lpc = int(m["kind"]) == abi.KIND_LPC
-    put.uint(0, 1)
-    put.uint((0b100000 | (order - 1)) if lpc else (0b001000 | order), 6)
-    put.uint(0, 1)
-    for s in samples[:order]:
-        put.uint(int(s), sample_size)
-    if lpc:
-        assert precision - 1 != 0b1111
-        put.uint(precision - 1, 4)
-        put.uint(int(m["shift"]), 5)
-        for c in m["coefs"][: int(m["ncoefs"])]:
-            put.uint(int(c), precision)
-    off, ln = int(m["res_offset"]), int(m["res_len"])
-    _put_residual(put, zz_row[off:off + ln], params_row[: int(m["n_parts"])], n, order,
-                  int(m["part_order"]), int(m["coding_method"]))
-
-
-def _frame(index: int, n: int, channels: int, sample_size: int, precision: int, rows: np.ndarray,
-           out: dict, u0: int) -> bytes:
-    put = put_frame_header(FrameHeader(blocking_strategy=BlockingStrategy.Fixed, block_size=n,
-                                       sample_rate=None, channels=Channels.L_R, sample_size=None,
-                                       coded_number=index))
-    for c in range(channels):
-        u = u0 + c
-        m = out["meta"][u]
-        _raise_for(m)
-        _put_subframe(put, rows[u], m, out["residual"][u], out["rice_params"][u], n, sample_size,
-                      precision)
-    put.uint(0, put.bits_until_alignment)
-    put.uint(crc16(put.buffer, CRC16_POLYNOMIAL), 16)
-    return put.buffer
-
-
 def encode(sample_rate: int, sample_size: int, channels: int, frames: int,
            samples: Iterator[list], parameters: EncoderParameters, *, device: int = 0,
            blocks_per_batch: int = 2048, fixed_only: bool = False) -> Iterator[bytes]:
-    """flac/encoder.py:48-165 with the per-channel analysis on the GPU.
+    """flac/encoder.py:48-165 on the GPU: the per-channel analysis (k_lpc, k_resid) and
+    the frame writer (k_frame.hip: Rice packing, headers, CRC-8/16).  Only the stream
+    header (magic + STREAMINFO) is written here.
 
     fixed_only=True selects fixed predictors only (BASELINE config 5); the reference
     has no such mode (its -l 0 raises ValueError, which the default mode reproduces)."""
@@ -253,11 +214,13 @@ def encode(sample_rate: int, sample_size: int, channels: int, frames: int,
 def _encode_batch(az, blocks, index0, channels, sample_size, parameters, params):
     n = parameters.block_size
     rows, bits, tail_len, n_tail = _planar(blocks, channels, n)
-    out = az.analyze(rows, params, n, tail_len, n_tail, sample_bits=bits)
+    data, offsets, status = az.encode_frames(rows, params, n, tail_len, n_tail, sample_bits=bits,
+                                             channels=channels, sample_size=sample_size, first_frame=index0)
+    buf = data.tobytes()
     for b in range(len(blocks)):
-        ln = len(blocks[b])
-        yield _frame(index0 + b, ln, channels, sample_size, parameters.qlp_precision, rows, out,
-                     b * channels)
+        st = int(status[b])
+        _raise_status(st & 0xFFFF, st >> 16)  # the reference raises after the frames before it
+        yield buf[int(offsets[b]):int(offsets[b + 1])]
 
 
 # ---------------------------------------------------------------------------------

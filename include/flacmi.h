@@ -81,7 +81,14 @@ enum flacmi_site {
     FLACMI_SITE_RICE_LOG_DOMAIN = 12,/* encoder.py:753  log2(0): partition sum is 0 */
     FLACMI_SITE_RICE_NEG_SHIFT = 13, /* encoder.py:758  1 << parameter, parameter < 0 */
     FLACMI_SITE_RESIDUAL_WIDTH = 14, /* not a reference site: see FLACMI_STATUS_RESIDUAL_WIDE */
+    /* frame writer (flacmi_frame_sizes_device): statements of the reference's writer */
+    FLACMI_SITE_CODED_NUMBER = 15,   /* coded_number.py:38  frame number needs more than 31 bits (ValueError) */
+    FLACMI_SITE_LPC_PRECISION = 16,  /* encoder.py:619  assert precision - 1 != 0b1111 (AssertionError) */
+    FLACMI_SITE_FRAME_SIZE = 17,     /* not a reference site: see FLACMI_STATUS_FRAME_TOO_LARGE */
 };
+
+/* frame writer status beyond the reference's exceptions */
+#define FLACMI_STATUS_FRAME_TOO_LARGE 17 /* a frame of >= 2^28 bytes: this build does not pack it */
 
 /* ---- analysis modes -------------------------------------------------------------- */
 enum flacmi_mode {
@@ -182,6 +189,49 @@ int flacmi_analyze_device(flacmi_ctx* ctx, const flacmi_batch* batch,
 /* Host pointers; copies in and out, synchronous. */
 int flacmi_analyze_host(flacmi_ctx* ctx, const flacmi_batch* batch,
                         const flacmi_params* params, const flacmi_outputs* out);
+
+/* ---- frame writer: FLAC frames from the analysis results -------------------------- */
+/* The reference writes each frame on the host, bit by bit (encoder.py:87-165 frame loop;
+ * put_frame_header :194-234 with coded_number.py:7-39 and crc.py:18-31; _put_subframe_header
+ * :553-569; _put_subframe_fixed/_lpc :581-627; put_residual / put_rice_partition /
+ * put_rice_int :765-806; padding + CRC-16 footer :159-163).  These entry points produce
+ * the same bytes on the device: frame f of a batch holds the units
+ * [f*channels, (f+1)*channels) (one subframe per channel, in channel order); the last
+ * frame may be short (the batch's tail units).  Frames are byte-aligned and packed back
+ * to back in `out` at frame_offsets[f] .. frame_offsets[f+1]. */
+typedef struct flacmi_frame_params {
+    int32_t channels;        /* units per frame, 1..8 (encode()'s channels) */
+    int32_t sample_size;     /* bits per warm-up sample in the stream (encode()'s sample_size), 1..32 */
+    int32_t qlp_precision;   /* SubframeLPC.precision (EncoderParameters.qlp_precision) */
+    int32_t reserved0;
+    int64_t first_frame;     /* coded number of the batch's first frame (block index, encoder.py:97) */
+    int64_t reserved[2];
+} flacmi_frame_params;
+
+/* Frame sizes and their exclusive prefix sums (device pointers, enqueued on `stream`).
+ * frame_offsets[n_frames + 1] receives byte offsets (frame_offsets[n_frames] = total);
+ * frame_status[n_frames] receives 0, or (site << 16) | status of the first subframe (in
+ * channel order) the reference would fail on while analysing or writing the frame; such
+ * a frame gets size 0 and is not written.  meta / rice_params are analyze outputs for the
+ * same batch; n_frames = ceil(n_units / channels). */
+int flacmi_frame_sizes_device(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_frame_params* fp,
+                              const flacmi_unit_meta* meta, const int32_t* rice_params, int64_t params_stride,
+                              int64_t* frame_offsets, int32_t* frame_status, void* stream);
+/* Write every frame with status 0 into out[frame_offsets[f] ..) (device pointers).  The
+ * residual rows are the analyze outputs (zig-zag u32 or u64 rows, residual_bytes 4 or 8).
+ * out must hold frame_offsets[n_frames] bytes (checked on the device against out_capacity;
+ * on overflow nothing is written and frame_status[0] is set to FLACMI_STATUS_FRAME_TOO_LARGE). */
+int flacmi_pack_frames_device(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_frame_params* fp,
+                              const flacmi_unit_meta* meta, const int32_t* rice_params, int64_t params_stride,
+                              const void* residual, int32_t residual_bytes, int64_t residual_stride,
+                              const int64_t* frame_offsets, int32_t* frame_status, uint8_t* out,
+                              int64_t out_capacity, void* stream);
+/* Host form of analyze + frame sizes + pack (synchronous): host samples in; frame_offsets
+ * [n_frames + 1] and frame_status [n_frames] out.  The frame bytes stay in a context
+ * buffer until flacmi_encode_fetch copies them (frame_offsets[n_frames] bytes) to the host. */
+int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_params* params,
+                       const flacmi_frame_params* fp, int64_t* frame_offsets, int32_t* frame_status);
+int flacmi_encode_fetch(flacmi_ctx* ctx, uint8_t* out, int64_t bytes);
 
 /* ---- stream statistics (reduced across GPUs with one RCCL all-reduce) ------------- */
 #define FLACMI_STATS_WORDS 128
