@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--parity-units", type=int, default=64)
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-frames", action="store_true", help="skip the frame-writer measurement")
     return ap.parse_args()
 
 
@@ -90,6 +91,80 @@ def cpu_baseline(cfg, seconds, seed):
             "sample": f"{done} units x {cfg['n']} samples (synthetic units 0..{done - 1}), "
                       f"oracle/flac_oracle.c on {threads} host threads, {t_an:.1f} s; the reference "
                       f"Python itself measured 56.8k samples/s/core here (BASELINE.md)"}
+
+
+def frame_writer_leg(args, cfg, az, samples, meta, rparams, residual, pstride, units, sptr, check):
+    """FLAC frames from the timed batch's analysis (not part of the
+    metric, which is encode-analysis): k_frame_sizes + scan + k_pack, timed with HIP
+    events on the launch stream over a few calls; a sample of frames is checked against
+    the frame-writer oracle (oracle/frame_writer.py) on the device's own analysis."""
+    import numpy as np
+    import torch
+
+    from flac_amd import abi
+    from flac_amd.analysis import device_batch, frame_params
+
+    dev = samples.device
+    n, bits = cfg["n"], cfg["bits"]
+    C = cfg["channels"]
+    nf = units // C
+    sbytes = samples.element_size()
+    b = device_batch(samples.data_ptr(), sbytes, bits, samples.shape[1], nf * C, n)
+    fp = frame_params(C, bits, cfg["q"], 0)
+    off = torch.empty(nf + 1, dtype=torch.int64, device=dev)
+    st = torch.empty(nf, dtype=torch.int32, device=dev)
+    az.frame_sizes_device(b, fp, meta.data_ptr(), rparams.data_ptr(), pstride, off.data_ptr(), st.data_ptr(), sptr)
+    torch.cuda.synchronize(dev)
+    total = int(off[-1].item())
+    out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+
+    def call():
+        az.frame_sizes_device(b, fp, meta.data_ptr(), rparams.data_ptr(), pstride, off.data_ptr(), st.data_ptr(),
+                              sptr)
+        az.pack_frames_device(b, fp, meta.data_ptr(), rparams.data_ptr(), pstride, residual.data_ptr(), 4,
+                              residual.shape[1], off.data_ptr(), st.data_ptr(), out.data_ptr(), out.numel(), sptr)
+
+    call()
+    torch.cuda.synchronize(dev)
+    reps = 5
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    bad_status = int((st != 0).sum().item())
+    meta_np = meta[:, :].cpu().numpy().view(abi.META_DTYPE).reshape(units)
+    res_read = 4.0 * float(meta_np["res_len"].sum())
+    algo = res_read + total + units * 208 + 4.0 * float(meta_np["n_parts"].sum()) + 16.0 * nf
+    res = {"ms_per_call": ms, "frames": nf, "bytes_out": total, "bytes_per_sample": total / (nf * C * n),
+           "samples_per_s": nf * C * n / (ms * 1e-3), "algorithmic_GBs": algo / (ms * 1e-3) / 1e9,
+           "frames_with_status": bad_status,
+           "note": "k_frame_sizes + 3-kernel scan + k_pack per call; reads the zig-zag residual rows, writes "
+                   "byte-exact FLAC frames (headers, Rice codes, CRC-8/16)"}
+    if check:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import frame_writer as FW  # checker only
+        rng = np.random.default_rng(args.seed + 1)
+        pick = np.sort(rng.choice(nf, size=min(32, nf), replace=False))
+        offs = off.cpu().numpy()
+        rp_np = rparams.cpu().numpy() if units <= 65536 else None
+        bad = 0
+        for f in pick:
+            us = list(range(f * C, (f + 1) * C))
+            rows = samples[torch.as_tensor(us, device=dev)].cpu().numpy()[:, :n]
+            ms_ = [meta_np[u] for u in us]
+            zz = [residual[u].cpu().numpy().view(np.uint32)[int(m["res_offset"]):int(m["res_offset"]) + int(m["res_len"])]
+                  for u, m in zip(us, ms_)]
+            prm = [(rp_np[u] if rp_np is not None else rparams[u].cpu().numpy())[: int(m["n_parts"])]
+                   for u, m in zip(us, ms_)]
+            want = FW.frame(int(f), n, list(rows), ms_, zz, prm, bits, cfg["q"])
+            got = out[int(offs[f]):int(offs[f + 1])].cpu().numpy().tobytes()
+            bad += 0 if got == want else 1
+        res["parity"] = {"frames_checked": int(len(pick)), "mismatches": bad,
+                         "check": "bytes vs oracle/frame_writer.py on the device analysis"}
+    return res
 
 
 def shard_first_unit(rank, units_per_rank):
@@ -211,6 +286,11 @@ def main():
         parity = {"units_checked": int(len(pick)), "mismatches": bad,
                   "check": "meta, coefficients, zig-zag residual and Rice parameters bit-exact vs oracle"}
 
+    frames = None
+    if not args.no_frames:
+        frames = frame_writer_leg(args, cfg, az, samples, meta, rparams, residual, pstride, units, sptr,
+                                  rank == 0 and not args.no_parity)
+
     lpc_b, resid_b, pipe_b = algorithmic_bytes(cfg, meta_np, units)
     lpc_gbs = lpc_b / (kt["lpc_ms"] * 1e-3) / 1e9 if kt["lpc_ms"] > 0 else 0.0
     resid_gbs = resid_b / (kt["resid_ms"] * 1e-3) / 1e9 if kt["resid_ms"] > 0 else 0.0
@@ -251,6 +331,7 @@ def main():
                         "pipeline_GBs": pipe_b / (kt["call_ms"] * 1e-3) / 1e9 if kt["call_ms"] else 0.0,
                         "timed_calls": kt["calls"]},
             "cpu_baseline": cpu,
+            "frame_writer": frames,
             "parity": parity,
             "stream_stats": {"units": int(st[0]), "samples": int(st[1]), "rice_bits": int(st[2]),
                              "fixed": int(st[3]), "lpc": int(st[4]), "errors": int(st[65:80].sum())},

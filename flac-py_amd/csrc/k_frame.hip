@@ -450,15 +450,31 @@ __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
             int pp[8];
             uint32_t len[8];
             uint32_t tsum = 0;
-            int part = i0 / ps;
+            /* partition of each value: one division per chunk; with ps >= 8 a chunk meets
+             * at most one partition boundary */
+            const int part0 = i0 / ps;
+            const int bnd = (part0 + 1) * ps;
+            int pA = 0, pB = 0;
+            if (ch < nch && ps >= 8) {
+                pA = rp[part0 < m.n_parts ? part0 : m.n_parts - 1];
+                pB = (bnd < n && bnd <= i0 + 7) ? rp[part0 + 1] : pA;
+            }
+            int part = part0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int i = i0 + k;
                 const bool valid = ch < nch && i >= order && i < n;
-                while ((part + 1) * ps <= i) ++part;
+                int p;
+                if (ps >= 8) {
+                    p = i >= bnd ? pB : pA;
+                } else {
+                    while ((part + 1) * ps <= i) ++part;
+                    p = valid ? rp[part] : 0;
+                }
+                p = valid ? p : 0;
                 z[k] = valid ? zrow[i] : (ZT)0;
-                const int p = valid ? rp[part] : 0;
-                const bool first = valid && (i == order || (i == part * ps && i > order));
+                const bool first = valid && (i == order || (i > order && (i == bnd || i == part0 * ps ||
+                                                                          (ps < 8 && i == part * ps))));
                 pp[k] = first ? p | 0x100 : p;
                 const uint32_t qv = p >= (int)(8 * sizeof(ZT)) ? 0u : (uint32_t)(z[k] >> p);
                 len[k] = valid ? (first ? (uint32_t)method : 0u) + qv + 1u + (uint32_t)p : 0u;
@@ -481,24 +497,80 @@ __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
             }
             __syncthreads();
             const uint32_t tstart = tile_base + pre_w + v - tsum;
-            segment(tile_base + tot, [&]() {
-                uint32_t pos = tstart;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    if (len[k] != 0) {
-                        const int p = pp[k] & 0xFF;
-                        uint32_t at = pos;
-                        if (pp[k] & 0x100) {
-                            win_or(win, wb, at, (uint64_t)p & pmask_m, method);
-                            at += (uint32_t)method;
+            if constexpr (sizeof(ZT) == 4) {
+                /* this thread's codes are contiguous: assemble them in a 64-bit buffer and
+                 * OR whole words into the window (its first and last word are shared) */
+                segment(tile_base + tot, [&]() {
+                    const uint32_t wlo = wb, whi = wb + kWinWords;
+                    uint32_t pos = tstart, widx = tstart >> 5;
+                    uint64_t acc = 0;
+                    auto emit = [&](uint32_t wi, uint32_t val) __attribute__((always_inline)) {
+                        if (val != 0 && wi >= wlo && wi < whi) atomicOr(&win[wi - wlo], val);
+                    };
+                    /* v right-aligned, 1 <= w <= 32; keeps pos - 32*widx in [0, 32) */
+                    auto put = [&](uint32_t val, int w) __attribute__((always_inline)) {
+                        const int off = (int)(pos - 32u * widx);
+                        acc |= (uint64_t)val << (64 - off - w);
+                        pos += (uint32_t)w;
+                        if (pos - 32u * widx >= 32u) {
+                            emit(widx, (uint32_t)(acc >> 32));
+                            acc <<= 32;
+                            ++widx;
                         }
-                        const uint32_t qv = p >= (int)(8 * sizeof(ZT)) ? 0u : (uint32_t)(z[k] >> p);
-                        const uint64_t val = (1ull << p) | ((uint64_t)z[k] & ((1ull << p) - 1));
-                        win_or(win, wb, at + qv, val, p + 1);
-                        pos += len[k];
+                    };
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (len[k] != 0) {
+                            const int p = pp[k] & 0xFF;
+                            if (pp[k] & 0x100) put((uint32_t)p & (uint32_t)pmask_m, method);
+                            const uint32_t zk = (uint32_t)z[k];
+                            const uint32_t qv = p >= 32 ? 0u : zk >> p;
+                            if (qv != 0) { /* unary zeros */
+                                pos += qv;
+                                if (pos - 32u * widx >= 32u) {
+                                    emit(widx, (uint32_t)(acc >> 32));
+                                    acc = 0;
+                                    widx = pos >> 5;
+                                }
+                            }
+                            /* the one and the p low bits: p + 1 <= 32 bits */
+                            const uint32_t lowm = p >= 32 ? 0xFFFFFFFFu : ((1u << p) - 1u);
+                            if (p >= 32) { /* not reachable for 32-bit values (p <= 31); kept exact */
+                                put(1u, 1);
+                                pos += (uint32_t)(p - 32);
+                                if (pos - 32u * widx >= 32u) {
+                                    emit(widx, (uint32_t)(acc >> 32));
+                                    acc = 0;
+                                    widx = pos >> 5;
+                                }
+                                put(zk, 32);
+                            } else {
+                                put((1u << p) | (zk & lowm), p + 1);
+                            }
+                        }
                     }
-                }
-            });
+                    if (pos != 32u * widx) emit(widx, (uint32_t)(acc >> 32));
+                });
+            } else {
+                segment(tile_base + tot, [&]() {
+                    uint32_t pos = tstart;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        if (len[k] != 0) {
+                            const int p = pp[k] & 0xFF;
+                            uint32_t at = pos;
+                            if (pp[k] & 0x100) {
+                                win_or(win, wb, at, (uint64_t)p & pmask_m, method);
+                                at += (uint32_t)method;
+                            }
+                            const uint32_t qv = p >= (int)(8 * sizeof(ZT)) ? 0u : (uint32_t)(z[k] >> p);
+                            const uint64_t val = (1ull << p) | ((uint64_t)z[k] & ((1ull << p) - 1));
+                            win_or(win, wb, at + qv, val, p + 1);
+                            pos += len[k];
+                        }
+                    }
+                });
+            }
             tile_base += tot;
         }
     }
@@ -531,10 +603,15 @@ int64_t frame_scan_blocks(int64_t n_frames) { return (n_frames + kScanBlock - 1)
 
 hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     if (a.n_frames <= 0) return hipSuccess;
+    /* workgroup: 8-value chunks in as few full tiles of <= 256 threads as possible */
+    const int nch = (a.block_len + 7) / 8;
+    const int tiles = (nch + kPackThreads - 1) / kPackThreads;
+    int nt = 64 * ((nch + 64 * tiles - 1) / (64 * tiles));
+    nt = nt < 64 ? 64 : nt;
     if (a.residual_bytes == 8)
-        hipLaunchKernelGGL(k_pack<uint64_t>, dim3((unsigned)a.n_frames), dim3(kPackThreads), 0, s, a);
+        hipLaunchKernelGGL(k_pack<uint64_t>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, a);
     else
-        hipLaunchKernelGGL(k_pack<uint32_t>, dim3((unsigned)a.n_frames), dim3(kPackThreads), 0, s, a);
+        hipLaunchKernelGGL(k_pack<uint32_t>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, a);
     return hipGetLastError();
 }
 

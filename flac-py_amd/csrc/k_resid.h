@@ -109,8 +109,11 @@ struct CoefTables {
     static constexpr int NP = (LMAX + 2) / 2; /* pairs per order: taps x[i], x[i-1] .. x[i-LMAX] */
     static constexpr int PPAD = NP > 0 ? ((NP + 3) / 4) * 4 : 4;    /* padded to uint4 */
     static constexpr int CPAD = LMAX > 0 ? ((LMAX + 3) / 4) * 4 : 4;
-    static constexpr int BYTES = 16 * ((4 * LMAX * (PPAD + CPAD) + 12 * LMAX + 15) / 16);
+    /* MFMA tap table (f32): [16 predictor columns][kTapW], tap(jj) at jj + 4, jj in [-4, 16) */
+    static constexpr int TAPF_OFF = 16 * ((4 * LMAX * (PPAD + CPAD) + 12 * LMAX + 15) / 16);
+    static constexpr int BYTES = TAPF_OFF + 16 * 20 * 4;
 };
+constexpr int kTapW = 20;
 
 /* PATH_S16 candidate sums.  The dot chain of order p carries one extra tap, x[i] with
  * coefficient -2^sh, and starts from 2^31: t = 2^31 + pred - x[i]*2^sh.  That is exact in
@@ -302,73 +305,60 @@ __device__ __forceinline__ uint32_t mfma_block(const int16_t* xs16, int i0, int 
 }
 
 /* Sums for the fixed orders 1..4 and LPC orders 1..min(L,12) into red[wid][.] (the order-0
- * sum, sum|x|, comes from the staging pass). */
+ * sum, sum|x|, comes from the staging pass).  Lane (col, kb) needs the taps
+ * tap(jj), jj = 8 - 4kb + m, m = 0..6 of its predictor column (phase A's LDS table):
+ * B_rho[j] = (j < 4 ? 256 : 1) * tap(jj) with m = 3 + rho - (j & 3), static per j. */
 template <int LMAX>
-__device__ __forceinline__ void mfma_candidate_sums(const int16_t* xs16, const int32_t* cfl, const int32_t* lsh,
+__device__ __forceinline__ void mfma_candidate_sums(const int16_t* xs16, const float* tapf, const int32_t* lsh,
                                                     int L, int n, int lane, int wid, int nw,
                                                     unsigned long long* red, uint32_t sumx) {
-    using CT = CoefTables<LMAX>;
     constexpr int NSUM = 5 + LMAX;
     const int col = lane & 15, kb = lane >> 4;
     const bool lpc_col = col < 12;
-    /* this lane's predictor: coefficients cc[0..11] (zero past the order) and shift */
-    const bool lpc_live = lpc_col && col < L;
+    const bool lpc_live = lpc_col && col < L && col < LMAX;
     const int row = (col < LMAX ? col : LMAX - 1);
-    int cc[12];
+    float t[7];
     {
-        const int4v* cr = reinterpret_cast<const int4v*>(cfl + row * CT::CPAD);
-        static_for<(CT::CPAD < 12 ? CT::CPAD : 12) / 4>([&](auto G_) {
-            constexpr int g = G_;
-            const int4v v = cr[g];
-            static_for<4>([&](auto E_) {
-                constexpr int e = E_;
-                cc[4 * g + e] = v[e];
-            });
-        });
-        static_for<12>([&](auto J_) {
-            constexpr int j = J_;
-            if constexpr (j >= CT::CPAD) cc[j] = 0;
-        });
-        const int k = col - 11; /* fixed order k: c_j = (-1)^j C(k, j+1) */
-        const int f0 = k, f1 = -(k * (k - 1) / 2), f2 = k * (k - 1) * (k - 2) / 6,
-                  f3 = -(k * (k - 1) * (k - 2) * (k - 3) / 24);
-        static_for<12>([&](auto J_) {
-            constexpr int j = J_;
-            const int fv = j == 0 ? f0 : j == 1 ? f1 : j == 2 ? f2 : j == 3 ? f3 : 0;
-            cc[j] = lpc_live ? cc[j] : (lpc_col ? 0 : fv);
-        });
+        const float* tp = tapf + col * kTapW + (8 - 4 * kb) + 4;
+#pragma unroll
+        for (int m = 0; m < 7; ++m) t[m] = tp[m];
     }
-    const int sh = lpc_live ? lsh[row] : 0;
-    const int start = lpc_col ? (lpc_live ? lsh[LMAX + row] : 0) : col - 11;
-    const float inv = __uint_as_float((uint32_t)(127 - sh) << 23); /* 2^-sh */
-    /* tap value by jj = -1 - d: -1 for x[i] itself, c[jj] * 2^-sh for x[i-1-jj] */
-    auto tap = [&](int jj) -> float {
-        return jj == -1 ? -1.0f : (jj >= 0 && jj < 12) ? (float)cc[jj] * inv : 0.0f;
-    };
     half8 B[4];
     static_for<4>([&](auto R_) {
         constexpr int rho = R_;
-        static_for<8>([&](auto J_) {
-            constexpr int j = J_;
-            constexpr int jw = j & 3;                    /* window slot within the k-block */
-            /* slot w = 4kb + jw, d = w - 12 - rho, jj = -1 - d = 11 + rho - w */
-            const float v0 = tap(11 + rho - jw), v1 = tap(7 + rho - jw), v2 = tap(3 + rho - jw),
-                        v3 = tap(-1 + rho - jw);
-            const float v = kb == 0 ? v0 : kb == 1 ? v1 : kb == 2 ? v2 : v3;
-            B[rho][j] = (_Float16)(j < 4 ? 256.0f * v : v);
+        uint32_t w[4];
+        static_for<4>([&](auto P_) {
+            constexpr int pj = P_; /* halves 2pj, 2pj+1 */
+            constexpr int j0 = 2 * pj, j1 = 2 * pj + 1;
+            const float a0 = t[3 + rho - (j0 & 3)] * (j0 < 4 ? 256.0f : 1.0f);
+            const float a1 = t[3 + rho - (j1 & 3)] * (j1 < 4 ? 256.0f : 1.0f);
+            w[pj] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a0, a1));
         });
+        B[rho] = __builtin_bit_cast(half8, uint4{w[0], w[1], w[2], w[3]});
     });
+    const int sh = lpc_live ? lsh[row] : 0;
+    const int start = lpc_col ? (lpc_live ? lsh[LMAX + row] : 0) : col - 11;
+    const float inv = __uint_as_float((uint32_t)(127 - sh) << 23); /* 2^-sh */
     const float cinit = 0.5f * inv - 0.5f;
     const frag_cd C{cinit, cinit, cinit, cinit};
     const int eoff = 4 * (lane & 15) - 12 + 4 * kb;
-    uint64_t acc = 0;
     const uint32_t mb = kFloorMagicBits;
     const int nblk = (n + 63) >> 6;
-    for (int blk = wid; blk < nblk; blk += nw) {
-        const int i0 = blk << 6;
-        if (blk == 0 || i0 + 64 > n) acc += mfma_block<true>(xs16, i0, eoff, B, C, kb, start, n, mb);
-        else acc += mfma_block<false>(xs16, i0, eoff, B, C, kb, start, n, mb);
+    const int nfull = n >> 6; /* blocks 1 .. nfull-1 need no mask */
+    uint64_t acc = 0;
+    /* masked blocks: block 0 (warm-up samples) and a partial last block */
+    if (wid == 0) acc += mfma_block<true>(xs16, 0, eoff, B, C, kb, start, n, mb);
+    if (nblk > nfull && nblk > 1 && (nblk - 1) % nw == wid)
+        acc += mfma_block<true>(xs16, (nblk - 1) << 6, eoff, B, C, kb, start, n, mb);
+    /* unmasked blocks, two per iteration: every |r| < 2^22 under the exactness bound, so a
+     * pair's 32 values per lane sum below 2^27 */
+    int blk = 1 + ((wid - 1 + nw) % nw);
+    for (; blk + nw < nfull; blk += 2 * nw) {
+        const uint32_t s0 = mfma_block<false>(xs16, blk << 6, eoff, B, C, kb, start, n, mb);
+        const uint32_t s1 = mfma_block<false>(xs16, (blk + nw) << 6, eoff, B, C, kb, start, n, mb);
+        acc += s0 + s1;
     }
+    if (blk < nfull) acc += mfma_block<false>(xs16, blk << 6, eoff, B, C, kb, start, n, mb);
     acc += (uint64_t)__shfl_xor((unsigned long long)acc, 16);
     acc += (uint64_t)__shfl_xor((unsigned long long)acc, 32);
     const uint32_t sx = wave_sum_u32(sumx);
@@ -632,6 +622,30 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
             }
         }
     }
+    if constexpr (MF) {
+        /* MFMA tap table: column col < 12 is LPC order col+1 (c_jj * 2^-shift), 12..15 the
+         * fixed orders 1..4; tap(-1) = -1 is x[i] itself */
+        float* tapf = reinterpret_cast<float*>(smem + lay.coef + CT::TAPF_OFF);
+        if (do_lpc) {
+            for (int i = tid; i < 16 * kTapW; i += NT) {
+                const int col = i / kTapW, jj = i % kTapW - 4;
+                float v = 0.0f;
+                if (jj == -1) {
+                    v = -1.0f;
+                } else if (jj >= 0 && col < 12) {
+                    if (col < L && col < LMAX && jj <= col) {
+                        const int sh = rec[2 + col];
+                        v = (float)rec[2 + L + (col * (col + 1)) / 2 + jj] * __uint_as_float((uint32_t)(127 - sh) << 23);
+                    }
+                } else if (jj >= 0) {
+                    const int k = col - 11; /* fixed order k: c_jj = (-1)^jj C(k, jj+1) */
+                    const int f[4] = {k, -(k * (k - 1) / 2), k * (k - 1) * (k - 2) / 6, -(k * (k - 1) * (k - 2) * (k - 3) / 24)};
+                    v = jj < 4 ? (float)f[jj] : 0.0f;
+                }
+                tapf[i] = v;
+            }
+        }
+    }
     if (tid == 0) {
         misc[0] = 0x7fffffff;
         misc[1] = 0;
@@ -649,7 +663,9 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
 
     /* ---- phase B: sum|r| for fixed orders 0..4 and LPC orders 1..L ---- */
     if (use_mfma) {
-        if constexpr (MF) mfma_candidate_sums<LMAX>(xs16, cfl, lsh, L, n, lane, wid, nw, red, sumx);
+        if constexpr (MF)
+            mfma_candidate_sums<LMAX>(xs16, reinterpret_cast<const float*>(smem + lay.coef + CT::TAPF_OFF), lsh, L,
+                                      n, lane, wid, nw, red, sumx);
         if (a.stop_after == 2) return;
     } else {
     A acc[NSUM];

@@ -1,0 +1,17 @@
+# SQ counter passes (one rocprofv3 --pmc run each) over a short bench: issue/wait
+# breakdown, instruction mix, LDS behaviour.  Usage: bash tools/pmc.sh <tag> [bench args]
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+TAG=${1:-pmc}; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+ARGS="--units 200000 --steps 2 --warmup 1 --cpu-seconds 0 --no-parity $*"
+P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
+P2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS"
+P3="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INSTS_BRANCH SQ_LDS_ADDR_CONFLICT SQ_INSTS"
+i=0
+for P in "$P1" "$P2" "$P3"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 bench.py $ARGS > $OUT/p$i.json 2> $OUT/p$i.err || { echo "pass $i failed"; tail -5 $OUT/p$i.err; exit 1; }
+done
+python3 tools/pmc_summary.py $OUT > $OUT/summary.txt && cat $OUT/summary.txt
