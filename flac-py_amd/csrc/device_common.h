@@ -130,7 +130,7 @@ struct Decision {
     int coef[FLACMI_MAX_LPC_ORDER];
 };
 
-constexpr int kCPT = 4; /* max 8-sample chunks per thread */
+constexpr int kCPT = 3; /* max 8-sample chunks per thread */
 
 /* Per-unit result written field by field (no local struct: keeps the kernel scratch-free). */
 __device__ __forceinline__ void put_meta(flacmi_unit_meta* m, int status, int site, const Decision* d,

@@ -155,7 +155,7 @@ struct flacmi_ctx {
     double* d_log2thr = nullptr;
     int32_t* d_sintab = nullptr;
     std::map<int, double*> windows;
-    DevBuf rec, h_samples, h_meta, h_params, h_residual, h_acf, h_fs, h_ls, h_recs;
+    DevBuf rec, retry, h_samples, h_meta, h_params, h_residual, h_acf, h_fs, h_ls, h_recs;
     uint16_t* d_crc = nullptr;  /* CRC-16 slice tables [4][256] + power tables [28][512] */
     DevBuf scan, h_offsets, h_status, h_frames;
     int64_t frames_bytes = 0;   /* bytes of the last flacmi_encode_host call */
@@ -238,7 +238,7 @@ void flacmi_destroy(flacmi_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     for (auto& kv : ctx->windows) (void)hipFree(kv.second);
-    for (DevBuf* b : {&ctx->rec, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
+    for (DevBuf* b : {&ctx->rec, &ctx->retry, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
                       &ctx->h_fs, &ctx->h_ls, &ctx->h_recs, &ctx->scan, &ctx->h_offsets, &ctx->h_status,
                       &ctx->h_frames})
         if (b->p) (void)hipFree(b->p);
@@ -360,6 +360,8 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         if (int rc = ensure_buf(ctx->rec, sizeof(int32_t) * (size_t)rec_words * (size_t)(b->n_units > 0 ? b->n_units : 1)))
             return rc;
     }
+    /* fast-kernel retry list: a counter, then one batch index per unit */
+    if (int rc = ensure_buf(ctx->retry, sizeof(int64_t) * (size_t)(b->n_units + 2))) return rc;
     struct Cls {
         int64_t unit0, count;
         int n;
@@ -420,6 +422,8 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.lpc_sums = o->lpc_sums ? o->lpc_sums + cls[c].unit0 * 32 : nullptr;
         a.stop_after = debug_stop();
         a.mfma = use_mfma();
+        a.retry_count = (unsigned long long*)ctx->retry.p;
+        a.retry_list = (int64_t*)ctx->retry.p + 2;
         const bool wide = needs_wide(cls[c].n, b->sample_bits, L, p->qlp_precision, p->mode);
         const int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
         HIP_TRY(launch_resid(a, path, o->residual_bytes, s));

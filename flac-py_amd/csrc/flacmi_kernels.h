@@ -46,7 +46,11 @@ struct ResidArgs {
                                 1 = after staging, 2 = after candidate sums, 3 = after the
                                 choice, 4 = after the chosen residual */
     int32_t mfma;            /* 1 = MFMA candidate sums where exact (env FLACMI_NO_MFMA=1 -> 0) */
+    unsigned long long* retry_count; /* fast-path units handed to the generic kernel: count, */
+    int64_t* retry_list;             /* and their batch indices (NULL: no fast path) */
 };
+/* internal unit status between the fast and the generic k_resid (never returned) */
+#define FLACMI_STATUS_RETRY 0x7e
 
 /* Frame writer (k_frame.hip): frame f = units [f*channels, (f+1)*channels). */
 struct FrameArgs {

@@ -369,6 +369,36 @@ __device__ __forceinline__ void mfma_candidate_sums(const int16_t* xs16, const f
     if (lane == 0) red[wid * NSUM] = sx;
 }
 
+/* Phase E of the fast kernel for a fixed predictor of order K (encoder.py:331-359,
+ * common.py:15-21): the residual of samples i0..i0+7 is their K-th difference, zig-zagged
+ * (utils.py:91-94); the warm-up samples i < K give 0.  16-bit samples: |r| < 2^19. */
+template <int K>
+__device__ __forceinline__ void fixed_resid_chunk(const int16_t* xs16, int i0, uint32_t (&z)[8]) {
+    const uint4 w = *reinterpret_cast<const uint4*>(xs16 + i0);
+    uint4 v{0, 0, 0, 0};
+    if constexpr (K > 0) v = *reinterpret_cast<const uint4*>(xs16 + i0 - 8); /* history pad >= 8 */
+    const uint32_t q[6] = {v.z, v.w, w.x, w.y, w.z, w.w};
+    int32_t d[12]; /* samples i0-4 .. i0+7 */
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        d[2 * t] = (int32_t)(q[t] << 16) >> 16;
+        d[2 * t + 1] = (int32_t)q[t] >> 16;
+    }
+#pragma unroll
+    for (int l = 1; l <= K; ++l)
+#pragma unroll
+        for (int t = 11; t >= 4 - K + l; --t) d[t] -= d[t - 1];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t r = d[4 + k];
+        z[k] = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+    }
+    if (i0 == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) z[k] = 0;
+    }
+}
+
 /* floor(log2(x)) for a Rice mean x (normal, > 0): LDS thresholds, global table outside. */
 __device__ __forceinline__ int rice_floor_log2(double x, const double* tl, const double* gthr) {
     const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
@@ -491,8 +521,21 @@ __device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta
     for (int K = tid; K < (1 << best); K += NT) rp[K] = pk[16 * (K << (omax - best)) + best];
 }
 
-template <int LMAX, int PATH, typename ResT>
+/* One unit per workgroup.  VAR selects the variant:
+ *   kVarGeneric  unit = blockIdx.x, every path;
+ *   kVarFast     unit = blockIdx.x, only the S16 MFMA path with a register-resident
+ *                residual (smaller register footprint: more workgroups per CU); a unit
+ *                outside the MFMA exactness bound is marked FLACMI_STATUS_RETRY and listed;
+ *   kVarList     unit = retry_list[blockIdx.x] for blockIdx.x < *retry_count, every path. */
+enum { kVarGeneric = 0, kVarFast = 1, kVarList = 2 };
+template <int LMAX, int PATH, typename ResT, int VAR>
 __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
+    constexpr bool FAST = VAR == kVarFast;
+    int64_t gid = blockIdx.x;
+    if constexpr (VAR == kVarList) {
+        if (gid >= (int64_t)*a.retry_count) return;
+        gid = a.retry_list[gid];
+    }
     using UX = ResT;
     constexpr bool S16 = PATH == PATH_S16;
     constexpr bool WIDE = PATH == PATH_W64;
@@ -501,23 +544,24 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     constexpr int HP = resid_hp(LMAX);
     constexpr int NSUM = 5 + LMAX;
     constexpr bool MF = S16 && (LMAX == 8 || LMAX == 12); /* MFMA candidate sums available */
+    static_assert(!FAST || (MF && sizeof(ResT) == 4), "FAST: S16 MFMA path with a 32-bit residual only");
 
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, wid = tid >> 6, nw = NT >> 6;
-    const int64_t gid = blockIdx.x;
     const int64_t u = a.unit0 + gid;
     const int n = a.n, L = a.L;
     const int nch = (n + 7) >> 3;
     /* LPC records exist in the reference and LPC-only modes */
-    const bool ref_mode = a.mode == FLACMI_MODE_REFERENCE || a.mode == FLACMI_MODE_LPC_ONLY;
-    const bool do_lpc = LMAX > 0 && ref_mode;
-    const bool rice_only = a.mode == FLACMI_MODE_RICE_ONLY;
+    const bool ref_mode = FAST || a.mode == FLACMI_MODE_REFERENCE || a.mode == FLACMI_MODE_LPC_ONLY;
+    const bool do_lpc = FAST || (LMAX > 0 && ref_mode);
+    const bool rice_only = !FAST && a.mode == FLACMI_MODE_RICE_ONLY;
+    const bool lpc_only = !FAST && a.mode == FLACMI_MODE_LPC_ONLY;
 
     /* ---- LDS carve (integer offsets keep every access a ds_* instruction) ---- */
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (n % (1 << o) == 0) rmax_eff = o;
-    const bool regz = resid_regz(n, rmax_eff, !WIDE && sizeof(ResT) == 4);
+    const bool regz = FAST || resid_regz(n, rmax_eff, !WIDE && sizeof(ResT) == 4);
     const ResidLds lay = resid_lds_layout(LMAX, n, nw, 1 << (rmax_eff < 0 ? 0 : rmax_eff), S16 ? 2 : 4,
                                           (int)sizeof(ResT), CT::BYTES, regz, false);
     int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
@@ -662,12 +706,20 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     if (a.stop_after == 1) return;
 
     /* ---- phase B: sum|r| for fixed orders 0..4 and LPC orders 1..L ---- */
+    if (FAST && !use_mfma) { /* outside the MFMA exactness bound: the generic kernel redoes it */
+        if (tid == 0) {
+            meta->status = FLACMI_STATUS_RETRY;
+            const unsigned long long k = atomicAdd(a.retry_count, 1ull);
+            a.retry_list[k] = gid;
+        }
+        return;
+    }
     if (use_mfma) {
         if constexpr (MF)
             mfma_candidate_sums<LMAX>(xs16, reinterpret_cast<const float*>(smem + lay.coef + CT::TAPF_OFF), lsh, L,
                                       n, lane, wid, nw, red, sumx);
         if (a.stop_after == 2) return;
-    } else {
+    } else if constexpr (!FAST) {
     A acc[NSUM];
 #pragma unroll
     for (int s = 0; s < NSUM; ++s) acc[s] = 0;
@@ -767,7 +819,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
                     }
                 }
             });
-            if (a.mode == FLACMI_MODE_LPC_ONLY) {
+            if (lpc_only) {
                 kind = FLACMI_KIND_LPC;
                 dorder = lbest;
                 dshift = lsh[lbest - 1];
@@ -916,11 +968,22 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
         if (regz) {
             /* register-resident residual: chunk c = tid + j*NT, j < kCPT */
             uint32_t zr[kCPT][8];
+            const int fixed_order = __builtin_amdgcn_readfirstlane(dec->kind == FLACMI_KIND_FIXED ? order : -1);
 #pragma unroll
             for (int j = 0; j < kCPT; ++j) {
                 const int c = tid + j * NT;
                 if (c < nch) {
-                    resid_chunk(c, zr[j]);
+                    if (FAST && fixed_order >= 0) { /* n % 8 == 0 here: every chunk is whole */
+                        switch (fixed_order) {
+                            case 0: fixed_resid_chunk<0>(xs16, 8 * c, zr[j]); break;
+                            case 1: fixed_resid_chunk<1>(xs16, 8 * c, zr[j]); break;
+                            case 2: fixed_resid_chunk<2>(xs16, 8 * c, zr[j]); break;
+                            case 3: fixed_resid_chunk<3>(xs16, 8 * c, zr[j]); break;
+                            default: fixed_resid_chunk<4>(xs16, 8 * c, zr[j]); break;
+                        }
+                    } else {
+                        resid_chunk(c, zr[j]);
+                    }
                     store_chunk(c, zr[j]);
                     cs[c] = zr[j][0] + zr[j][1] + zr[j][2] + zr[j][3] + zr[j][4] + zr[j][5] + zr[j][6] + zr[j][7];
                 } else {
@@ -930,7 +993,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
             }
             __syncthreads();
             if (a.stop_after == 4) return;
-            if (a.mode == FLACMI_MODE_LPC_ONLY) {
+            if (lpc_only) {
                 lpc_only_done();
                 return;
             }
@@ -966,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
             return;
         }
     }
-
+    if constexpr (!FAST) {
 #pragma unroll 1
     for (int c = tid; c < nch; c += NT) {
         ResT zv[8];
@@ -1129,6 +1192,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     const int best = misc[3];
     int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
     for (int K = tid; K < (1 << best); K += NT) rp[K] = hp[(1 << best) + K];
+    } /* !FAST */
 }
 
 template <int LMAX, int PATH, typename ResT>
@@ -1141,16 +1205,53 @@ static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff),
                                         PATH == PATH_S16 ? 2 : 4, (int)sizeof(ResT), CoefTables<LMAX>::BYTES,
                                         regz, false).total;
-    auto kern = k_resid<LMAX, PATH, ResT>;
+    auto kern = k_resid<LMAX, PATH, ResT, kVarGeneric>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)a.count), dim3(nt), lds, s, a);
     return hipGetLastError();
 }
 
+/* S16 MFMA fast kernel over the batch, then the generic body over the units it listed */
+template <int LMAX>
+static hipError_t launch_resid_fast(const ResidArgs& a, hipStream_t s) {
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (a.n % (1 << o) == 0) rmax_eff = o;
+    const int nt = resid_threads(a.n);
+    const int P = 1 << (rmax_eff < 0 ? 0 : rmax_eff);
+    const size_t lds_fast = resid_lds_layout(LMAX, a.n, nt / 64, P, 2, 4, CoefTables<LMAX>::BYTES, true, false).total;
+    const size_t lds_gen = resid_lds_layout(LMAX, a.n, nt / 64, P, 2, 4, CoefTables<LMAX>::BYTES, true, false).total;
+    hipError_t e = hipMemsetAsync(a.retry_count, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    auto kf = k_resid<LMAX, PATH_S16, uint32_t, kVarFast>;
+    e = hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fast);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kf, dim3((unsigned)a.count), dim3(nt), lds_fast, s, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    /* the listed units: one workgroup each; the rest of the grid exits on the count */
+    auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
+    e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gen);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kl, dim3((unsigned)a.count), dim3(nt), lds_gen, s, a);
+    return hipGetLastError();
+}
+
+/* the fast kernel's preconditions: reference mode, 32-bit narrow residual kept in
+ * registers (resid_regz), MFMA enabled, a retry list to hand exceptions to */
+static inline bool resid_fast_ok(const ResidArgs& a) {
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (a.n % (1 << o) == 0) rmax_eff = o;
+    return a.mode == FLACMI_MODE_REFERENCE && a.mfma && a.retry_list && a.retry_count &&
+           resid_regz(a.n, rmax_eff, true);
+}
+
 template <int LMAX>
 static hipError_t launch_resid_bucket(const ResidArgs& a, int path, int rb, hipStream_t s) {
     if (rb == 8) return launch_resid_T<LMAX, PATH_W64, uint64_t>(a, s);
+    if constexpr (LMAX == 8 || LMAX == 12)
+        if (path == PATH_S16 && resid_fast_ok(a)) return launch_resid_fast<LMAX>(a, s);
     if (path == PATH_S16) return launch_resid_T<LMAX, PATH_S16, uint32_t>(a, s);
     if (path == PATH_N32) return launch_resid_T<LMAX, PATH_N32, uint32_t>(a, s);
     return launch_resid_T<LMAX, PATH_W64, uint32_t>(a, s);

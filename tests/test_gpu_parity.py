@@ -107,6 +107,15 @@ def test_c2_shape_batch(az):
     batch_case(az, 192, 4608, 16, 2024, 12, 5, 0, 5)
 
 
+@pytest.mark.parametrize("q", [6, 7, 9, 15])
+def test_c2_shape_fast_kernel_and_retry_list(az, q):
+    """config 2 shape at higher precisions: the fast S16 MFMA kernel takes the units inside
+    its exactness bound (sum|c| + 2^shift <= 127) and hands the rest to the generic kernel
+    through the retry list; q = 15 sends every LPC unit there."""
+    batch_case(az, 96, 4608, 16, 300 + q, 12, q, 0, 5)
+    batch_case(az, 64, 4608, 16, 400 + q, 8, q, 0, 5)
+
+
 def test_c1_params_with_short_tail(az):
     """config 1 parameters with a stream's short last block (3240 samples)."""
     batch_case(az, 40, 4608, 16, 7, 8, 5, 0, 5, tail=(3240, 1))
