@@ -416,6 +416,7 @@ __device__ __forceinline__ int rice_floor_log2(double x, const double* tl, const
  *  2. every thread, per chunk it owns: sum over the chunk of x >> p for each candidate
  *     order, parameters from pk of the chunk's finest partition (chunk_rice_bits);
  *  3. one wave reduction per order; thread 0 picks the order, first minimum (rice_finish). */
+template <bool INTLOG>
 __device__ __forceinline__ void rice_params_wave0(const ResidArgs& a, uint64_t s, const double* tl,
                                                   unsigned long long* rb, int* misc, uint8_t* pk, int n, int order,
                                                   int rmin, int omax, int lane) {
@@ -432,7 +433,19 @@ __device__ __forceinline__ void rice_params_wave0(const ResidArgs& a, uint64_t s
         const bool zero = s == 0;
         bool neg = false;
         if (!zero) {
-            prm = rice_floor_log2((double)s / (double)len, tl, a.log2thr);
+            if constexpr (INTLOG) {
+                /* exact integer floor(log2(s/len)) = max{p : len * 2^p <= s}.  For s < 2^46 and
+                 * len < 2^16 the reference's float division + libm log2 give the same value:
+                 * the quotient is at least a relative 2^-46 away from the next power of two,
+                 * far outside the rounding of the division and of log2. */
+                const int fs = 63 - __builtin_clzll((unsigned long long)s);
+                const int fl = 31 - __builtin_clz((unsigned)len);
+                int p = fs - fl;
+                if (p >= 0 && ((uint64_t)len << p) > s) --p;
+                prm = p;
+            } else {
+                prm = rice_floor_log2((double)s / (double)len, tl, a.log2thr);
+            }
             neg = prm < 0;
         }
         if (k < P) pk[16 * k + o] = (uint8_t)prm;
@@ -584,6 +597,82 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     /* ---- phase A: stage samples and the candidate coefficients ---- */
     uint32_t sumx = 0; /* this thread's sum|x| (MFMA path: the fixed order-0 sum) */
     int mf_ok = 1;     /* this thread's orders pass the MFMA exactness bound */
+    /* FAST: one global round trip.  The samples and the LPC record are loaded together;
+     * the record is staged in LDS (in the chunk-sum region, free until phase E), and every
+     * table is built from there after one barrier. */
+    bool use_mfma = false;
+    if constexpr (FAST) {
+        int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.cs);
+        const int16_t* __restrict__ src = (const int16_t*)a.samples + u * a.stride;
+        int32_t rw = 0;
+        if (tid < a.rec_words) rw = rec[tid];
+        for (int i = tid; i < HP; i += NT) xs16[i - HP] = 0;
+        for (int i = n + tid; i < resid_xpad(n); i += NT) xs16[i] = 0;
+        for (int v = tid; v < (n >> 3); v += NT) { /* n % 8 == 0 */
+            const uint4 q = *reinterpret_cast<const uint4*>(src + 8 * v);
+            *reinterpret_cast<uint4*>(xs16 + 8 * v) = q;
+            const uint32_t qd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int32_t x0 = (int32_t)(qd[e] << 16) >> 16, x1 = (int32_t)qd[e] >> 16;
+                sumx += (uint32_t)(x0 < 0 ? -x0 : x0) + (uint32_t)(x1 < 0 ? -x1 : x1);
+            }
+        }
+        if (tid < a.rec_words) recl[tid] = rw;
+        if (tid == 0) {
+            misc[0] = 0x7fffffff;
+            misc[1] = 0;
+            misc[2] = 0;
+        }
+        if (tid < 32) rb[tid] = 0;
+        __syncthreads();
+        const int st = recl[0];
+        if (st != 0) { /* the reference raises inside encode_subframe_lpc */
+            if (tid == 0) put_meta(meta, st & 0xffff, st >> 16, nullptr, 0);
+            return;
+        }
+        const uint32_t negmask = (uint32_t)recl[1];
+        for (int i = tid; i < LMAX * CT::CPAD; i += NT) {
+            const int pp = i / CT::CPAD + 1, j = i % CT::CPAD;
+            cfl[i] = (pp <= L && j < pp) ? recl[2 + L + (pp * (pp - 1)) / 2 + j] : 0;
+        }
+        for (int i = tid; i < LMAX; i += NT) {
+            const int sh = i < L ? recl[2 + i] : 0; /* 0..15 */
+            lsh[i] = sh;
+            lsh[LMAX + i] = ((negmask >> i) & 1) ? 0 : i + 1; /* first residual index */
+            lsh[2 * LMAX + i] = (int32_t)(1u << (31 - sh));
+            if (i < L) {
+                const int32_t* cp = recl + 2 + L + (i * (i + 1)) / 2;
+                int sa = 1 << sh;
+#pragma unroll
+                for (int j = 0; j < LMAX; ++j)
+                    if (j <= i) sa += cp[j] < 0 ? -cp[j] : cp[j];
+                mf_ok &= sa <= kMfmaCoefLimit;
+            }
+        }
+        /* MFMA tap table: column col < 12 is LPC order col+1 (c_jj * 2^-shift), 12..15 the
+         * fixed orders 1..4; tap(-1) = -1 is x[i] itself */
+        float* tapf = reinterpret_cast<float*>(smem + lay.coef + CT::TAPF_OFF);
+        for (int i = tid; i < 16 * kTapW; i += NT) {
+            const int col = i / kTapW, jj = i % kTapW - 4;
+            float v = 0.0f;
+            if (jj == -1) {
+                v = -1.0f;
+            } else if (jj >= 0 && col < 12) {
+                if (col < L && col < LMAX && jj <= col) {
+                    const int sh = recl[2 + col];
+                    v = (float)recl[2 + L + (col * (col + 1)) / 2 + jj] * __uint_as_float((uint32_t)(127 - sh) << 23);
+                }
+            } else if (jj >= 0) {
+                const int k = col - 11; /* fixed order k: c_jj = (-1)^jj C(k, jj+1) */
+                const int f[4] = {k, -(k * (k - 1) / 2), k * (k - 1) * (k - 2) / 6, -(k * (k - 1) * (k - 2) * (k - 3) / 24)};
+                v = jj < 4 ? (float)f[jj] : 0.0f;
+            }
+            tapf[i] = v;
+        }
+        use_mfma = __syncthreads_and(mf_ok) && a.mfma;
+    } else {
+
     if (ref_mode) {
         const int st = rec[0];
         if (st != 0) { /* the reference raises inside encode_subframe_lpc */
@@ -697,11 +786,11 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     }
     if (tid < 32) rb[tid] = 0;
     if (tid < 64) tl[tid] = a.log2thr[tid + kTlLo + 1074];
-    bool use_mfma = false;
     if constexpr (MF) {
         use_mfma = __syncthreads_and(mf_ok) && do_lpc && a.mfma;
     } else {
         __syncthreads();
+    }
     }
     if (a.stop_after == 1) return;
 
@@ -1007,9 +1096,12 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
             uint8_t* pk = reinterpret_cast<uint8_t*>(hs);
             if (wid == 0) {
                 uint64_t s = 0;
-                if (lane < (1 << omax))
+                if (lane < (1 << omax)) {
+#pragma unroll 6
                     for (int c = lane * cpp; c < (lane + 1) * cpp; ++c) s += cs[c];
-                rice_params_wave0(a, s, tl, rb, misc, pk, n, order, a.rmin, omax, lane);
+                }
+                /* FAST: residual < 2^27 and n <= 6144, so every partition sum < 2^40 */
+                rice_params_wave0<FAST>(a, s, tl, rb, misc, pk, n, order, a.rmin, omax, lane);
             }
             __syncthreads();
             if (misc[0] >= 0) {
@@ -1077,7 +1169,7 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
                         s += (uint64_t)(u.x + u.y + u.z + u.w + v.x + v.y + v.z + v.w);
                     }
                 }
-                rice_params_wave0(a, s, tl, rb, misc, pk, n, order, rmin, omax, lane);
+                rice_params_wave0<false>(a, s, tl, rb, misc, pk, n, order, rmin, omax, lane);
             }
             __syncthreads();
             if (misc[0] >= 0) {
@@ -1243,8 +1335,9 @@ static inline bool resid_fast_ok(const ResidArgs& a) {
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
+    /* the record is staged in the chunk-sum region during phase A */
     return a.mode == FLACMI_MODE_REFERENCE && a.mfma && a.retry_list && a.retry_count &&
-           resid_regz(a.n, rmax_eff, true);
+           resid_regz(a.n, rmax_eff, true) && (a.n + 7) / 8 + 1 >= a.rec_words;
 }
 
 template <int LMAX>
