@@ -155,12 +155,18 @@ struct flacmi_ctx {
     double* d_log2thr = nullptr;
     int32_t* d_sintab = nullptr;
     std::map<int, double*> windows;
+    std::map<int, std::pair<int, int>> window_one; /* per n: [lo, hi) where the weight is 1.0 */
     DevBuf rec, retry, h_samples, h_meta, h_params, h_residual, h_acf, h_fs, h_ls, h_recs;
     uint16_t* d_crc = nullptr;  /* CRC-16 slice tables [4][256] + power tables [28][512] */
     DevBuf scan, h_offsets, h_status, h_frames;
     int64_t frames_bytes = 0;   /* bytes of the last flacmi_encode_host call */
-    static constexpr int kRing = 256;
-    hipEvent_t ev[kRing][3] = {};
+    static constexpr int kRing = 64;
+    static constexpr int kMaxChunks = 8;
+    /* per call: start, LPC done, residual done, then (overlap) per chunk the k_resid start/end */
+    hipEvent_t ev[kRing][3 + 2 * kMaxChunks] = {};
+    int nchunks[kRing] = {};
+    hipStream_t side = nullptr;          /* k_lpc stream of the overlap mode */
+    hipEvent_t lpc_done[kMaxChunks] = {}; /* k_lpc of chunk i finished (no timing) */
     int ncalls = 0; /* calls since the last timing reset */
 };
 
@@ -220,6 +226,8 @@ flacmi_ctx* flacmi_create(int device) {
     for (auto& slot : ctx->ev)
         for (auto& ev : slot)
             if ((e = hipEventCreate(&ev)) != hipSuccess) return bad(e, "hipEventCreate");
+    for (auto& ev : ctx->lpc_done)
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipMalloc(&ctx->d_log2thr, sizeof(double) * PYM_LOG2_THR_N)) != hipSuccess) return bad(e, "hipMalloc");
     if ((e = hipMemcpy(ctx->d_log2thr, g_log2thr.data(), sizeof(double) * PYM_LOG2_THR_N, hipMemcpyHostToDevice)) != hipSuccess)
         return bad(e, "hipMemcpy");
@@ -249,23 +257,43 @@ void flacmi_destroy(flacmi_ctx* ctx) {
         for (auto& ev : slot)
             if (ev) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
+    for (auto& ev : ctx->lpc_done)
+        if (ev) (void)hipEventDestroy(ev);
     delete ctx;
 }
 
 }  // extern "C"
 
-static int get_window(flacmi_ctx* ctx, int n, double** out) {
+static int get_window(flacmi_ctx* ctx, int n, double** out, int* one_lo = nullptr, int* one_hi = nullptr) {
     auto it = ctx->windows.find(n);
-    if (it != ctx->windows.end()) {
-        *out = it->second;
-        return 0;
+    if (it == ctx->windows.end()) {
+        std::vector<double> w = tukey_window(n, 64);
+        double* d = nullptr;
+        HIP_TRY(hipMalloc(&d, sizeof(double) * w.size()));
+        HIP_TRY(hipMemcpy(d, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice));
+        ctx->windows[n] = d;
+        /* the longest run of weights exactly 1.0 (the rectangle of encoder.py:433) */
+        int best_lo = 0, best_hi = 0;
+        for (int i = 0; i < n;) {
+            if (w[i] != 1.0) {
+                ++i;
+                continue;
+            }
+            int j = i;
+            while (j < n && w[j] == 1.0) ++j;
+            if (j - i > best_hi - best_lo) {
+                best_lo = i;
+                best_hi = j;
+            }
+            i = j;
+        }
+        ctx->window_one[n] = {best_lo, best_hi};
+        it = ctx->windows.find(n);
     }
-    std::vector<double> w = tukey_window(n, 64);
-    double* d = nullptr;
-    HIP_TRY(hipMalloc(&d, sizeof(double) * w.size()));
-    HIP_TRY(hipMemcpy(d, w.data(), sizeof(double) * w.size(), hipMemcpyHostToDevice));
-    ctx->windows[n] = d;
-    *out = d;
+    *out = it->second;
+    if (one_lo) *one_lo = ctx->window_one[n].first;
+    if (one_hi) *one_hi = ctx->window_one[n].second;
     return 0;
 }
 
@@ -350,6 +378,17 @@ static int use_mfma() {
     return v;
 }
 
+/* FLACMI_OVERLAP=k (k > 1): k_lpc and k_resid of consecutive chunks overlap on two
+ * streams (see analyze_device_impl); chunks hold at least kOverlapMinUnits units. */
+constexpr int64_t kOverlapMinUnits = 16384;
+static int overlap_chunks() {
+    static const int v = [] {
+        const char* e = getenv("FLACMI_OVERLAP");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi_params* p,
                                const flacmi_outputs* o, hipStream_t s) {
     if (int rc = set_device(ctx)) return rc;
@@ -376,57 +415,106 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
     }
     if (o->acf && !lpc)
         HIP_TRY(hipMemsetAsync(o->acf, 0, sizeof(double) * 33 * b->n_units, s));
-    hipEvent_t* ev = ctx->ev[ctx->ncalls % flacmi_ctx::kRing];
-    HIP_TRY(hipEventRecord(ev[0], s));
-    /* LPC analysis for every class first, then the residual pass */
-    for (int c = 0; c < ncls && lpc; ++c) {
-        LpcArgs a{};
+    /* Units in chunks of one class each.  Without overlap: one chunk per class, the LPC
+     * pass over all of them, then the residual pass, in order on s.  With overlap
+     * (FLACMI_OVERLAP=k > 1): each class in up to k chunks; k_lpc runs the chunks in order
+     * on the side stream and k_resid of chunk i (on s) waits only for k_lpc of chunk i, so
+     * the f64 autocorrelation of chunk i+1 shares the GPU with the integer/MFMA work of
+     * chunk i. */
+    struct Chunk {
+        int64_t unit0, count;
+        int n;
+    } ch[flacmi_ctx::kMaxChunks];
+    int nch = 0;
+    const int want = lpc && overlap_chunks() > 1 ? overlap_chunks() : 1;
+    const bool overlap = want > 1 && b->n_units >= 2 * kOverlapMinUnits;
+    for (int c = 0; c < ncls; ++c) {
+        int64_t k = overlap ? cls[c].count / kOverlapMinUnits : 1;
+        const int left = flacmi_ctx::kMaxChunks - nch - (ncls - 1 - c);
+        k = k < 1 ? 1 : k > want ? want : k;
+        k = k > left ? left : k;
+        for (int64_t i = 0; i < k; ++i) {
+            const int64_t u0 = cls[c].count * i / k, u1 = cls[c].count * (i + 1) / k;
+            ch[nch++] = {cls[c].unit0 + u0, u1 - u0, cls[c].n};
+        }
+    }
+    auto lpc_args = [&](const Chunk& k, LpcArgs& a) -> int {
+        a = LpcArgs{};
         a.samples = b->samples;
         a.stride = b->unit_stride;
-        a.unit0 = cls[c].unit0;
-        a.count = cls[c].count;
+        a.unit0 = k.unit0;
+        a.count = k.count;
         a.sample_bytes = b->sample_bytes;
-        a.n = cls[c].n;
+        a.n = k.n;
         a.L = L;
         a.q = p->qlp_precision;
-        if (int rc = get_window(ctx, cls[c].n, (double**)&a.window)) return rc;
+        if (int rc = get_window(ctx, k.n, (double**)&a.window, &a.fuse_lo, &a.fuse_hi)) return rc;
+        if (b->sample_bits > 26) a.fuse_lo = a.fuse_hi = 0; /* products must stay below 2^52 */
         a.log2thr = ctx->d_log2thr;
-        a.rec = (int32_t*)ctx->rec.p + cls[c].unit0 * rec_words;
+        a.rec = (int32_t*)ctx->rec.p + k.unit0 * rec_words;
         a.rec_words = rec_words;
-        a.acf = o->acf ? o->acf + cls[c].unit0 * 33 : nullptr;
-        HIP_TRY(launch_lpc(a, s));
-    }
-    HIP_TRY(hipEventRecord(ev[1], s));
-    for (int c = 0; c < ncls; ++c) {
+        a.acf = o->acf ? o->acf + k.unit0 * 33 : nullptr;
+        return 0;
+    };
+    auto launch_resid_chunk = [&](const Chunk& k, hipStream_t st) -> hipError_t {
         ResidArgs a{};
         a.samples = b->samples;
         a.stride = b->unit_stride;
-        a.unit0 = cls[c].unit0;
-        a.count = cls[c].count;
+        a.unit0 = k.unit0;
+        a.count = k.count;
         a.sample_bytes = b->sample_bytes;
-        a.n = cls[c].n;
+        a.n = k.n;
         a.L = L;
         a.mode = p->mode;
         a.rmin = p->rice_min;
         a.rmax = p->rice_max;
-        a.rec = lpc ? (const int32_t*)ctx->rec.p + cls[c].unit0 * rec_words : nullptr;
+        a.rec = lpc ? (const int32_t*)ctx->rec.p + k.unit0 * rec_words : nullptr;
         a.rice_order = p->mode == FLACMI_MODE_RICE_ONLY ? p->reserved[0] : 0;
         a.rec_words = rec_words;
         a.log2thr = ctx->d_log2thr;
-        a.meta = o->meta + cls[c].unit0;
-        a.rice_params = o->rice_params + cls[c].unit0 * o->params_stride;
+        a.meta = o->meta + k.unit0;
+        a.rice_params = o->rice_params + k.unit0 * o->params_stride;
         a.params_stride = o->params_stride;
-        a.residual = (char*)o->residual + (size_t)cls[c].unit0 * o->residual_stride * o->residual_bytes;
+        a.residual = (char*)o->residual + (size_t)k.unit0 * o->residual_stride * o->residual_bytes;
         a.residual_stride = o->residual_stride;
-        a.fixed_sums = o->fixed_sums ? o->fixed_sums + cls[c].unit0 * 5 : nullptr;
-        a.lpc_sums = o->lpc_sums ? o->lpc_sums + cls[c].unit0 * 32 : nullptr;
+        a.fixed_sums = o->fixed_sums ? o->fixed_sums + k.unit0 * 5 : nullptr;
+        a.lpc_sums = o->lpc_sums ? o->lpc_sums + k.unit0 * 32 : nullptr;
         a.stop_after = debug_stop();
         a.mfma = use_mfma();
         a.retry_count = (unsigned long long*)ctx->retry.p;
         a.retry_list = (int64_t*)ctx->retry.p + 2;
-        const bool wide = needs_wide(cls[c].n, b->sample_bits, L, p->qlp_precision, p->mode);
+        const bool wide = needs_wide(k.n, b->sample_bits, L, p->qlp_precision, p->mode);
         const int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
-        HIP_TRY(launch_resid(a, path, o->residual_bytes, s));
+        return launch_resid(a, path, o->residual_bytes, st);
+    };
+    const int slot = ctx->ncalls % flacmi_ctx::kRing;
+    hipEvent_t* ev = ctx->ev[slot];
+    ctx->nchunks[slot] = overlap ? nch : 0;
+    HIP_TRY(hipEventRecord(ev[0], s));
+    if (overlap) {
+        if (!ctx->side) HIP_TRY(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+        HIP_TRY(hipStreamWaitEvent(ctx->side, ev[0], 0));
+        for (int i = 0; i < nch; ++i) {
+            LpcArgs a;
+            if (int rc = lpc_args(ch[i], a)) return rc;
+            HIP_TRY(launch_lpc(a, ctx->side));
+            HIP_TRY(hipEventRecord(ctx->lpc_done[i], ctx->side));
+        }
+        HIP_TRY(hipEventRecord(ev[1], ctx->side));
+        for (int i = 0; i < nch; ++i) {
+            HIP_TRY(hipStreamWaitEvent(s, ctx->lpc_done[i], 0));
+            HIP_TRY(hipEventRecord(ev[3 + 2 * i], s));
+            HIP_TRY(launch_resid_chunk(ch[i], s));
+            HIP_TRY(hipEventRecord(ev[4 + 2 * i], s));
+        }
+    } else {
+        for (int i = 0; i < nch && lpc; ++i) {
+            LpcArgs a;
+            if (int rc = lpc_args(ch[i], a)) return rc;
+            HIP_TRY(launch_lpc(a, s));
+        }
+        HIP_TRY(hipEventRecord(ev[1], s));
+        for (int i = 0; i < nch; ++i) HIP_TRY(launch_resid_chunk(ch[i], s));
     }
     HIP_TRY(hipEventRecord(ev[2], s));
     ctx->ncalls++;
@@ -758,8 +846,16 @@ int flacmi_last_timing(flacmi_ctx* ctx, float* ms, int n) {
         float t;
         HIP_TRY(hipEventElapsedTime(&t, ev[0], ev[1]));
         acc[0] += t;
-        HIP_TRY(hipEventElapsedTime(&t, ev[1], ev[2]));
-        acc[1] += t;
+        const int nk = ctx->nchunks[c % flacmi_ctx::kRing];
+        if (nk == 0) {
+            HIP_TRY(hipEventElapsedTime(&t, ev[1], ev[2]));
+            acc[1] += t;
+        } else { /* overlap: the k_resid launches' own spans */
+            for (int i = 0; i < nk; ++i) {
+                HIP_TRY(hipEventElapsedTime(&t, ev[3 + 2 * i], ev[4 + 2 * i]));
+                acc[1] += t;
+            }
+        }
         HIP_TRY(hipEventElapsedTime(&t, ev[0], ev[2]));
         acc[2] += t;
     }

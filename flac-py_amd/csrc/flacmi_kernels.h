@@ -22,6 +22,8 @@ struct LpcArgs {
     int32_t* rec;            /* [count][rec_words] LPC records (workspace) */
     int32_t rec_words;
     double* acf;             /* optional [count][33] */
+    int32_t fuse_lo, fuse_hi; /* window[i] == 1.0 exactly for i in [fuse_lo, fuse_hi) and
+                                 |x| < 2^26 (0, 0: no fused blocks), see k_lpc */
 };
 
 struct ResidArgs {

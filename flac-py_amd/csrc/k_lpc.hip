@@ -8,32 +8,6 @@ namespace flacmi {
  * k_lpc: autocorrelation + Levinson-Durbin + quantisation, one lane per unit
  * ==================================================================================== */
 
-/* Load S consecutive samples starting at m0 (S multiple of 8, 16-byte aligned). */
-template <int S, typename SampleT>
-__device__ __forceinline__ void load_block(const SampleT* __restrict__ x, int m0, int M, bool full,
-                                           int32_t (&v)[S]) {
-    if (full) {
-        if constexpr (sizeof(SampleT) == 2) {
-#pragma unroll
-            for (int g = 0; g < S / 8; ++g) {
-                const short8 s = *reinterpret_cast<const short8*>(x + m0 + 8 * g);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) v[8 * g + k] = s[k];
-            }
-        } else {
-#pragma unroll
-            for (int g = 0; g < S / 4; ++g) {
-                const int4v s = *reinterpret_cast<const int4v*>(x + m0 + 4 * g);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) v[4 * g + k] = s[k];
-            }
-        }
-    } else {
-#pragma unroll
-        for (int t = 0; t < S; ++t) v[t] = (m0 + t < M) ? (int32_t)x[m0 + t] : 0;
-    }
-}
-
 template <int LMAX>
 __device__ __forceinline__ void write_quant(int32_t* rec, int L, int p, const int32_t* q, int nq,
                                             int shift) {
@@ -70,26 +44,78 @@ __global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
 #pragma unroll
     for (int l = 0; l <= LMAX; ++l) acc[l] = 0.0;
     const int M = n - 1; /* the last sample never enters a product (encoder.py:449) */
-    const int nblk = (M + S - 1) / S;
     const double* __restrict__ win = a.window;
-    int32_t cur[S];
-    if (nblk > 0) load_block<S>(x, 0, M, S <= M, cur);
+    /* Samples arrive in load blocks of SB per lane (64 B: a whole half cache line per row
+     * per visit), kept packed (int16 pairs) and prefetched one block ahead; each block is
+     * processed as SB / S ring-aligned sub-blocks of S samples. */
+    constexpr int PK = sizeof(SampleT) == 2 ? 2 : 1; /* samples per 32-bit word */
+    constexpr int SB = sizeof(SampleT) == 2 ? 2 * S : S;
+    constexpr int W = SB / PK;
+    const int nblk = (M + SB - 1) / SB;
+    uint32_t cur[W];
+    auto load = [&](int m0, uint32_t (&v)[W]) __attribute__((always_inline)) {
+        if (m0 + SB <= M) {
+#pragma unroll
+            for (int g = 0; g < W / 4; ++g) {
+                const uint4 q = *reinterpret_cast<const uint4*>(x + m0 + 4 * PK * g);
+                v[4 * g] = q.x;
+                v[4 * g + 1] = q.y;
+                v[4 * g + 2] = q.z;
+                v[4 * g + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                if constexpr (PK == 2) {
+                    const uint32_t lo = (m0 + 2 * w < M) ? (uint16_t)x[m0 + 2 * w] : 0u;
+                    const uint32_t hi = (m0 + 2 * w + 1 < M) ? (uint16_t)x[m0 + 2 * w + 1] : 0u;
+                    v[w] = lo | (hi << 16);
+                } else {
+                    v[w] = (m0 + w < M) ? (uint32_t)x[m0 + w] : 0u;
+                }
+            }
+        }
+    };
+    auto sample = [&](const uint32_t (&v)[W], int t) __attribute__((always_inline)) -> int32_t {
+        if constexpr (PK == 2) return (t & 1) ? (int32_t)v[t >> 1] >> 16 : (int32_t)(v[t >> 1] << 16) >> 16;
+        return (int32_t)v[t];
+    };
+    if (nblk > 0) load(0, cur);
     for (int b = 0; b < nblk; ++b) {
-        const int m0 = b * S;
-        int32_t nxt[S];
-        if (b + 1 < nblk) load_block<S>(x, m0 + S, M, m0 + 2 * S <= M, nxt);
+        const int mb = b * SB;
+        uint32_t nxt[W];
+        if (b + 1 < nblk) load(mb + SB, nxt);
 #pragma unroll
-        for (int t = 0; t < S; ++t) {
-            const double av = (double)cur[t] * win[m0 + t];
-            ring[t] = av;
+        for (int sb = 0; sb < SB / S; ++sb) {
+            const int m0 = mb + sb * S;
+            if (m0 - LMAX >= a.fuse_lo && m0 + S <= a.fuse_hi) {
+                /* Inside the Tukey window's rectangle (weight exactly 1.0) every windowed
+                 * sample and lag partner is the integer sample itself, and the product of two
+                 * integers below 2^26 is exact in a double: RN(acc + RN(p * a)) ==
+                 * fma(p, a, acc).  One fused op per term instead of a multiply and an add,
+                 * bit-identical. */
 #pragma unroll
-            for (int l = 0; l <= LMAX; ++l) {
-                const double prev = ring[(t - l + S) % S];
-                acc[l] = acc[l] + prev * av;
+                for (int t = 0; t < S; ++t) {
+                    const double av = (double)sample(cur, sb * S + t);
+                    ring[t] = av;
+#pragma unroll
+                    for (int l = 0; l <= LMAX; ++l) acc[l] = __builtin_fma(ring[(t - l + S) % S], av, acc[l]);
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < S; ++t) {
+                    const double av = (double)sample(cur, sb * S + t) * win[m0 + t];
+                    ring[t] = av;
+#pragma unroll
+                    for (int l = 0; l <= LMAX; ++l) {
+                        const double prev = ring[(t - l + S) % S];
+                        acc[l] = acc[l] + prev * av;
+                    }
+                }
             }
         }
 #pragma unroll
-        for (int t = 0; t < S; ++t) cur[t] = nxt[t];
+        for (int w = 0; w < W; ++w) cur[w] = nxt[w];
     }
     if (a.acf) {
         double* o = a.acf + gid * 33;
