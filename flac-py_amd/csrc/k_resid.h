@@ -304,6 +304,27 @@ __device__ __forceinline__ uint32_t mfma_block(const int16_t* xs16, int i0, int 
     return bs[0] + bs[1] + bs[2] + bs[3];
 }
 
+/* an unmasked block accumulated into the caller's four running sums (no per-block
+ * reduction; the caller bounds how many blocks share them) */
+__device__ __forceinline__ void mfma_block_acc(const int16_t* xs16, int i0, int eoff, const half8 (&B)[4],
+                                               const frag_cd& C, uint32_t mb, uint32_t (&bs)[4]) {
+    const uint2 q = *reinterpret_cast<const uint2*>(xs16 + i0 + eoff);
+    const uint4 av{f16_hi_bytes(q.x), f16_hi_bytes(q.y), f16_lo_bytes(q.x), f16_lo_bytes(q.y)};
+    const half8 A = __builtin_bit_cast(half8, av);
+    frag_cd D[4];
+    static_for<4>([&](auto R_) {
+        constexpr int rho = R_;
+        D[rho] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[rho], C, 0, 0, 0);
+    });
+    static_for<4>([&](auto R_) {
+        constexpr int rho = R_;
+        static_for<4>([&](auto Q_) {
+            constexpr int r = Q_;
+            bs[r] = sad_u32(__float_as_uint(D[rho][r] + kFloorMagic), mb, bs[r]);
+        });
+    });
+}
+
 /* Sums for the fixed orders 1..4 and LPC orders 1..min(L,12) into red[wid][.] (the order-0
  * sum, sum|x|, comes from the staging pass).  Lane (col, kb) needs the taps
  * tap(jj), jj = 8 - 4kb + m, m = 0..6 of its predictor column (phase A's LDS table):
@@ -350,15 +371,15 @@ __device__ __forceinline__ void mfma_candidate_sums(const int16_t* xs16, const f
     if (wid == 0) acc += mfma_block<true>(xs16, 0, eoff, B, C, kb, start, n, mb);
     if (nblk > nfull && nblk > 1 && (nblk - 1) % nw == wid)
         acc += mfma_block<true>(xs16, (nblk - 1) << 6, eoff, B, C, kb, start, n, mb);
-    /* unmasked blocks, two per iteration: every |r| < 2^22 under the exactness bound, so a
-     * pair's 32 values per lane sum below 2^27 */
+    /* unmasked blocks in groups of up to 16 per wave: every |r| < 2^22 under the exactness
+     * bound, so each of the four running sums (64 values) stays below 2^28 */
     int blk = 1 + ((wid - 1 + nw) % nw);
-    for (; blk + nw < nfull; blk += 2 * nw) {
-        const uint32_t s0 = mfma_block<false>(xs16, blk << 6, eoff, B, C, kb, start, n, mb);
-        const uint32_t s1 = mfma_block<false>(xs16, (blk + nw) << 6, eoff, B, C, kb, start, n, mb);
-        acc += s0 + s1;
+    while (blk < nfull) {
+        uint32_t bs[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 2
+        for (int g = 0; g < 16 && blk < nfull; ++g, blk += nw) mfma_block_acc(xs16, blk << 6, eoff, B, C, mb, bs);
+        acc += (uint64_t)((bs[0] + bs[1]) + (bs[2] + bs[3]));
     }
-    if (blk < nfull) acc += mfma_block<false>(xs16, blk << 6, eoff, B, C, kb, start, n, mb);
     acc += (uint64_t)__shfl_xor((unsigned long long)acc, 16);
     acc += (uint64_t)__shfl_xor((unsigned long long)acc, 32);
     const uint32_t sx = wave_sum_u32(sumx);
@@ -560,7 +581,8 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     static_assert(!FAST || (MF && sizeof(ResT) == 4), "FAST: S16 MFMA path with a 32-bit residual only");
 
     extern __shared__ __align__(16) unsigned char smem[];
-    const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, wid = tid >> 6, nw = NT >> 6;
+    const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, nw = NT >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6); /* wave-uniform: scalar loops */
     const int64_t u = a.unit0 + gid;
     const int n = a.n, L = a.L;
     const int nch = (n + 7) >> 3;
