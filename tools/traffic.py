@@ -8,6 +8,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -19,11 +20,21 @@ def rows(pattern):
     return out
 
 
+STAGES = ("k_resid", "k_lpc", "k_stats", "k_synth", "k_pack", "k_frame_sizes", "k_decode")
+
+
 def short(name):
-    for k in ("k_resid", "k_lpc", "k_stats", "k_synth"):
-        if k in name:
+    """Full kernel name without the argument list, e.g. 'k_resid<12, 0, unsigned int, 1>'."""
+    name = name.split("(")[0]
+    name = name[5:] if name.startswith("void ") else name
+    return name.replace("flacmi::", "")[:60]
+
+
+def stage(name):
+    for k in STAGES:
+        if re.match(k + r"\b", short(name)):
             return k
-    return name[:40]
+    return None
 
 
 def main(d):
@@ -42,7 +53,14 @@ def main(d):
     for k, v in res["kernels"].items():
         if "fetch_size_bytes" in v and "write_size_bytes" in v:
             v["hbm_bytes_per_launch"] = v["fetch_size_bytes"] + v["write_size_bytes"]
-            res[k] = v["hbm_bytes_per_launch"]
+    # A stage (e.g. k_resid: the MFMA variant plus its retry launch) is timed as one HIP
+    # event interval by the library, so its traffic is the sum over its variants.
+    for k, v in res["kernels"].items():
+        st = stage(k)
+        if st and "hbm_bytes_per_launch" in v:
+            res[st] = res.get(st, 0.0) + v["hbm_bytes_per_launch"]
+            res.setdefault("stage_avg_ms", {})
+            res["stage_avg_ms"][st] = res["stage_avg_ms"].get(st, 0.0) + v.get("avg_ms", 0.0)
     print(json.dumps(res, indent=1))
 
 
