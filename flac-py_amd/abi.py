@@ -26,12 +26,15 @@ STATUS_VALUE_ERROR = 3
 STATUS_OVERFLOW = 4
 STATUS_RESIDUAL_WIDE = 16
 STATUS_FRAME_TOO_LARGE = 17
+STATUS_EOF = 5          # EOFError (decoder)
+STATUS_VERIFY = 18      # decoder verifier finding, not a reference exception
 
 STATUS_EXCEPTION = {
     STATUS_ZERO_DIVISION: ZeroDivisionError,
     STATUS_ASSERTION: AssertionError,
     STATUS_VALUE_ERROR: ValueError,
     STATUS_OVERFLOW: OverflowError,
+    STATUS_EOF: EOFError,
 }
 
 # flacmi_site
@@ -150,6 +153,25 @@ class FrameParams(C.Structure):
     ]
 
 
+class DecodeParams(C.Structure):
+    _fields_ = [
+        ("channels", C.c_int32),
+        ("sample_size", C.c_int32),
+        ("first_frame", C.c_int64),
+        ("check_crc", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("reserved", C.c_int64 * 2),
+    ]
+
+
+# flacmi_decode_site (frame_status >> 16 of flacmi_decode_frames_device)
+DSITE = {name: 32 + i for i, name in enumerate((
+    "sync", "block_size_code", "sample_rate_code", "channels_code", "sample_size_code", "reserved",
+    "subframe_pad", "subframe_type", "lpc_precision", "coding_method", "partitions", "escape_zero",
+    "neg_shift", "padding", "eof", "crc8", "crc16", "frame_end", "frame_number", "block_size", "channels",
+    "samples"))}
+
+
 # Every symbol include/flacmi.h declares, with its ctypes signature.
 SIGNATURES = {
     "flacmi_abi_version": (C.c_int, []),
@@ -169,6 +191,9 @@ SIGNATURES = {
     "flacmi_encode_host": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Params), C.POINTER(FrameParams),
                                      C.c_void_p, C.c_void_p]),
     "flacmi_encode_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "flacmi_decode_frames_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                                              C.POINTER(DecodeParams), C.POINTER(Batch), C.c_void_p, C.c_int64,
+                                              C.c_void_p, C.c_void_p, C.c_void_p]),
     "flacmi_stream_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
                                       C.c_int64, C.c_void_p, C.c_void_p]),
     "flacmi_synth_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,

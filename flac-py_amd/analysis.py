@@ -196,6 +196,50 @@ class Analyzer:
                                                  offsets_ptr, status_ptr, out_ptr, capacity, stream),
               "flacmi_pack_frames_device")
 
+    # ------------------------------------------------------------------------------
+    # decoder verifier (include/flacmi.h flacmi_decode_frames_device)
+    # ------------------------------------------------------------------------------
+    def decode_frames_device(self, data_ptr: int, data_bytes: int, offsets_ptr: int, n_frames: int,
+                             dp: abi.DecodeParams, expect: abi.Batch = None, out_ptr: int = 0,
+                             out_stride: int = 0, status_ptr: int = 0, mismatch_ptr: int = 0,
+                             stream: int = 0) -> None:
+        check(self.lib.flacmi_decode_frames_device(self.ctx, data_ptr, data_bytes, offsets_ptr, n_frames,
+                                                   C.byref(dp), C.byref(expect) if expect is not None else None,
+                                                   out_ptr or None, out_stride, status_ptr, mismatch_ptr, stream),
+              "flacmi_decode_frames_device")
+
+    def decode_frames(self, data: np.ndarray, offsets: np.ndarray, channels: int, sample_size: int,
+                      first_frame: int = -1, expect: np.ndarray = None, block_len: int = 0, tail_len: int = 0,
+                      n_tail_units: int = 0, out_stride: int = 0, check_crc: bool = True):
+        """Host bytes in -> (decoded int32 rows [n_frames*channels][out_stride], frame status,
+        mismatches per frame), decoded on the device.  `expect` (int16/int32 rows of the
+        source units) turns on the in-kernel comparison."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        n_frames = len(offsets) - 1
+        nb = int(len(data))
+        buf = torch.zeros(((nb + 3) // 4) * 4 + 16, dtype=torch.uint8, device=dev)
+        if nb:
+            buf[:nb] = torch.from_numpy(np.array(data, dtype=np.uint8, copy=True)).to(dev)
+        off = torch.from_numpy(np.ascontiguousarray(offsets, dtype=np.int64)).to(dev)
+        if out_stride <= 0:
+            out_stride = ((max(block_len, 1) + 3) // 4) * 4
+        out = torch.zeros((max(n_frames * channels, 1), out_stride), dtype=torch.int32, device=dev)
+        st = torch.zeros(max(n_frames, 1), dtype=torch.int32, device=dev)
+        mm = torch.zeros(max(n_frames, 1), dtype=torch.int64, device=dev)
+        dp = abi.DecodeParams()
+        dp.channels, dp.sample_size, dp.first_frame, dp.check_crc = channels, sample_size, first_frame, int(check_crc)
+        eb = None
+        if expect is not None:
+            e = torch.from_numpy(np.ascontiguousarray(expect)).to(dev)
+            eb = device_batch(e.data_ptr(), e.element_size(), 16 if e.element_size() == 2 else 32, e.shape[1],
+                              e.shape[0], block_len, tail_len, n_tail_units)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        self.decode_frames_device(buf.data_ptr(), nb, off.data_ptr(), n_frames, dp, eb, out.data_ptr(), out_stride,
+                                  st.data_ptr(), mm.data_ptr(), stream)
+        torch.cuda.synchronize(dev)
+        return out.cpu().numpy(), st.cpu().numpy()[:n_frames], mm.cpu().numpy()[:n_frames]
+
     def timing(self) -> dict:
         """Average k_lpc / k_resid / whole-call milliseconds over the analyze calls since
         the last timing_reset() (HIP events recorded on each call's stream)."""

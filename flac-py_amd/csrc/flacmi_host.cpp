@@ -158,7 +158,7 @@ struct flacmi_ctx {
     std::map<int, std::pair<int, int>> window_one; /* per n: [lo, hi) where the weight is 1.0 */
     DevBuf rec, retry, h_samples, h_meta, h_params, h_residual, h_acf, h_fs, h_ls, h_recs;
     uint16_t* d_crc = nullptr;  /* CRC-16 slice tables [4][256] + power tables [28][512] */
-    DevBuf scan, h_offsets, h_status, h_frames;
+    DevBuf scan, h_offsets, h_status, h_frames, dec;
     int64_t frames_bytes = 0;   /* bytes of the last flacmi_encode_host call */
     static constexpr int kRing = 64;
     static constexpr int kMaxChunks = 8;
@@ -246,7 +246,7 @@ void flacmi_destroy(flacmi_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     for (auto& kv : ctx->windows) (void)hipFree(kv.second);
-    for (DevBuf* b : {&ctx->rec, &ctx->retry, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
+    for (DevBuf* b : {&ctx->dec, &ctx->rec, &ctx->retry, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
                       &ctx->h_fs, &ctx->h_ls, &ctx->h_recs, &ctx->scan, &ctx->h_offsets, &ctx->h_status,
                       &ctx->h_frames})
         if (b->p) (void)hipFree(b->p);
@@ -691,6 +691,57 @@ int flacmi_pack_frames_device(flacmi_ctx* ctx, const flacmi_batch* batch, const 
     a.out = out;
     a.capacity = out_capacity;
     HIP_TRY(launch_pack(a, (hipStream_t)stream));
+    return 0;
+}
+
+int flacmi_decode_frames_device(flacmi_ctx* ctx, const uint8_t* stream_data, int64_t stream_bytes,
+                                const int64_t* frame_offsets, int64_t n_frames,
+                                const flacmi_decode_params* dp, const flacmi_batch* expect,
+                                int32_t* samples_out, int64_t out_stride, int32_t* frame_status,
+                                int64_t* frame_mismatch, void* stream) {
+    if (!ctx || !dp) return fail(FLACMI_E_INVALID, "null argument");
+    if (n_frames < 0 || stream_bytes < 0) return fail(FLACMI_E_INVALID, "negative size");
+    if (n_frames == 0) return 0;
+    if (!stream_data || !frame_offsets || !frame_status || !frame_mismatch) return fail(FLACMI_E_INVALID, "null buffer");
+    if (((uintptr_t)stream_data & 3) != 0) return fail(FLACMI_E_INVALID, "stream_data must be 4-byte aligned");
+    if (dp->channels < 1 || dp->channels > 8) return fail(FLACMI_E_INVALID, "channels must be 1..8");
+    if (dp->sample_size < 4 || dp->sample_size > 32) return fail(FLACMI_E_INVALID, "sample_size must be 4..32");
+    if (samples_out && (out_stride < 1 || (out_stride & 3) != 0 || ((uintptr_t)samples_out & 15) != 0))
+        return fail(FLACMI_E_INVALID, "samples_out rows must be 16-byte aligned (out_stride a multiple of 4)");
+    if (expect) {
+        if (expect->sample_bytes != 2 && expect->sample_bytes != 4) return fail(FLACMI_E_INVALID, "expect: sample_bytes 2 or 4");
+        if (expect->n_units != n_frames * dp->channels) return fail(FLACMI_E_INVALID, "expect: n_units != n_frames * channels");
+        if (expect->unit_stride < expect->block_len) return fail(FLACMI_E_INVALID, "expect: unit_stride < block_len");
+        if (expect->n_tail_units && expect->tail_len > expect->block_len) return fail(FLACMI_E_INVALID, "expect: tail_len > block_len");
+    }
+    if (int rc = set_device(ctx)) return rc;
+    if (int rc = ensure_buf(ctx->dec, sizeof(int32_t) * (size_t)n_frames)) return rc;
+    DecodeArgs a{};
+    a.words = reinterpret_cast<const uint32_t*>(stream_data);
+    a.stream_bytes = stream_bytes;
+    a.n_words = (stream_bytes + 3) / 4;
+    a.offsets = frame_offsets;
+    a.n_frames = n_frames;
+    a.channels = dp->channels;
+    a.sample_size = dp->sample_size;
+    a.first_frame = dp->first_frame;
+    a.check_crc = dp->check_crc;
+    if (expect) {
+        a.expect = expect->samples;
+        a.expect_stride = expect->unit_stride;
+        a.expect_bytes = expect->sample_bytes;
+        a.block_len = expect->block_len;
+        a.tail_len = expect->n_tail_units ? expect->tail_len : expect->block_len;
+        a.n_units = expect->n_units;
+        a.n_tail_units = expect->n_tail_units;
+    }
+    a.out = samples_out;
+    a.out_stride = out_stride;
+    a.status = frame_status;
+    a.mismatch = frame_mismatch;
+    a.decorr = (int32_t*)ctx->dec.p;
+    a.crc_slice = ctx->d_crc;
+    HIP_TRY(launch_decode(a, (hipStream_t)stream));
     return 0;
 }
 

@@ -77,6 +77,28 @@ struct FrameArgs {
     const uint16_t* crc_pow;   /* [28][512] multiply-by-x^(8*2^b) tables */
 };
 
+/* Decoder verifier (k_decode.hip): frame f = bytes [offsets[f], offsets[f+1]) of words. */
+struct DecodeArgs {
+    const uint32_t* words;   /* the stream as dwords (4-byte aligned base) */
+    int64_t stream_bytes, n_words;
+    const int64_t* offsets;  /* [n_frames + 1] */
+    int64_t n_frames;
+    int32_t channels, sample_size;
+    int64_t first_frame;
+    int32_t check_crc;
+    const void* expect;      /* optional source rows [n_frames*channels][expect_stride] */
+    int64_t expect_stride;
+    int32_t expect_bytes;
+    int32_t block_len, tail_len;
+    int64_t n_units, n_tail_units;
+    int32_t* out;            /* optional [n_frames*channels][out_stride] */
+    int64_t out_stride;
+    int32_t* status;         /* [n_frames] */
+    int64_t* mismatch;       /* [n_frames] */
+    int32_t* decorr;         /* [n_frames] scratch: (bs << 8) | channel code for k_decorr, else 0 */
+    const uint16_t* crc_slice; /* [4][256] CRC-16 slice-by-4 tables */
+};
+
 struct ResidLaunch {
     int threads;             /* workgroup size (multiple of 64) */
     size_t lds_bytes;        /* dynamic LDS */
@@ -102,6 +124,7 @@ hipError_t launch_stats(const flacmi_unit_meta* meta, int64_t n_units, int32_t b
 hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s);
 int64_t frame_scan_blocks(int64_t n_frames);
 hipError_t launch_pack(const FrameArgs& a, hipStream_t s);
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
 
 hipError_t launch_selftest(int32_t which, const double* x, double* out, int32_t* status, int64_t n,
                            const double* log2thr, hipStream_t s);

@@ -233,6 +233,70 @@ int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_
                        const flacmi_frame_params* fp, int64_t* frame_offsets, int32_t* frame_status);
 int flacmi_encode_fetch(flacmi_ctx* ctx, uint8_t* out, int64_t bytes);
 
+/* ---- decoder verifier (BASELINE config 5 round trip) ------------- */
+/* Replaces the reference's frame decoder: decoder.py:111-130 get_frame, :133-190
+ * get_frame_header (+ coded_number.py:45-70 decode), :192-245 field decoders, :267-344
+ * get_subframe / get_subframe_header / get_subframe_type, :346-355 get_wasted_bits, :358-421
+ * get_residual / get_rice_partition / get_rice_int, :431-498 decode_frame / decode_*_subframe
+ * / _decode_prediction.  Frame f is the bytes stream[frame_offsets[f] .. frame_offsets[f+1]).
+ * Per frame the device parses the header, every subframe and the footer, restores the
+ * samples and (optionally) compares them with the batch they were encoded from.
+ *
+ * frame_status[f] = (site << 16) | status: the exception the reference decoder raises
+ * (AssertionError / ValueError / EOFError, flacmi_decode_site names the statement), or a
+ * verifier finding the reference does not check (FLACMI_STATUS_VERIFY: CRC-8 / CRC-16,
+ * frame end, frame number, block size, sample mismatch).  frame_mismatch[f] counts the
+ * samples that differ from `expect` (0 when expect is NULL).  Decoding is byte-exact to
+ * the reference on every valid frame, with two documented choices: an L_R frame holds
+ * dp->channels subframes (encoder.py:95 writes L_R whatever the channel count, so the
+ * reference decoder cannot read back its own mono or 3+ channel streams), and, as in
+ * decode_subframe, wasted bits are parsed but not shifted back in. */
+#define FLACMI_STATUS_EOF 5        /* EOFError: the frame runs past the end of the stream */
+#define FLACMI_STATUS_VERIFY 18    /* verifier finding (not a reference exception) */
+enum flacmi_decode_site {
+    FLACMI_DSITE_SYNC = 32,          /* decoder.py:134  assert sync code */
+    FLACMI_DSITE_BLOCK_SIZE_CODE,    /* :194  assert 0 < block-size code < 15 */
+    FLACMI_DSITE_SAMPLE_RATE_CODE,   /* :213  assert sample-rate code < 15 */
+    FLACMI_DSITE_CHANNELS_CODE,      /* :232  assert channel code <= 10 */
+    FLACMI_DSITE_SAMPLE_SIZE_CODE,   /* :239  assert sample-size code != 3 */
+    FLACMI_DSITE_RESERVED,           /* :141  assert reserved bit == 0 */
+    FLACMI_DSITE_SUBFRAME_PAD,       /* :319  assert subframe padding bit == 0 */
+    FLACMI_DSITE_SUBFRAME_TYPE,      /* :329-331  assert reserved subframe type */
+    FLACMI_DSITE_LPC_PRECISION,      /* :302  assert precision != 0b1111 */
+    FLACMI_DSITE_CODING_METHOD,      /* :394  ValueError: cannot read coding method */
+    FLACMI_DSITE_PARTITIONS,         /* :363-364  assert block size / partition order */
+    FLACMI_DSITE_ESCAPE_ZERO,        /* binary.py:131 sint(0): ValueError negative shift count */
+    FLACMI_DSITE_NEG_SHIFT,          /* :496-497  ValueError: negative LPC shift in _decode_prediction */
+    FLACMI_DSITE_PADDING,            /* :126  assert frame padding == 0 */
+    FLACMI_DSITE_EOF,                /* binary.py:40  EOFError: the stream ends inside the frame */
+    FLACMI_DSITE_CRC8,               /* verifier: header CRC-8 mismatch (crc.py:18-22) */
+    FLACMI_DSITE_CRC16,              /* verifier: frame CRC-16 mismatch (crc.py:25-31) */
+    FLACMI_DSITE_FRAME_END,          /* verifier: the frame does not end at frame_offsets[f+1] */
+    FLACMI_DSITE_FRAME_NUMBER,       /* verifier: coded number != first_frame + f */
+    FLACMI_DSITE_BLOCK_SIZE,         /* verifier: block size != the expected unit length / out_stride */
+    FLACMI_DSITE_CHANNELS,           /* verifier: header channel count != dp->channels */
+    FLACMI_DSITE_SAMPLES,            /* verifier: decoded samples differ from `expect` */
+};
+typedef struct flacmi_decode_params {
+    int32_t channels;        /* subframes per frame (STREAMINFO channels), 1..8 */
+    int32_t sample_size;     /* STREAMINFO sample size, used when the header defers to it, 4..32 */
+    int64_t first_frame;     /* coded number expected for frame 0, or -1: not checked */
+    int32_t check_crc;       /* 1: verify CRC-8 and CRC-16 (the reference reads them unchecked) */
+    int32_t reserved0;
+    int64_t reserved[2];
+} flacmi_decode_params;
+/* All pointers are device pointers; the work is enqueued on `stream`.  stream_bytes is the
+ * readable size of `stream` (4-byte aligned base).  expect: NULL, or the batch whose unit
+ * f*channels + c the subframe c of frame f must reproduce (block_len / tail_len /
+ * n_tail_units give the expected block sizes).  samples_out: NULL, or int32 rows
+ * [n_frames*channels][out_stride] (out_stride a multiple of 4, 16-byte aligned rows) that
+ * receive the decoded samples; required when a frame uses L_S / S_R / M_S stereo. */
+int flacmi_decode_frames_device(flacmi_ctx* ctx, const uint8_t* stream_data, int64_t stream_bytes,
+                                const int64_t* frame_offsets, int64_t n_frames,
+                                const flacmi_decode_params* dp, const flacmi_batch* expect,
+                                int32_t* samples_out, int64_t out_stride, int32_t* frame_status,
+                                int64_t* frame_mismatch, void* stream);
+
 /* ---- stream statistics (reduced across GPUs with one RCCL all-reduce) ------------- */
 #define FLACMI_STATS_WORDS 128
 /* stats[0] units, [1] samples, [2] rice bits, [3] fixed units, [4] lpc units,

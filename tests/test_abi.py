@@ -33,7 +33,8 @@ def test_struct_layouts_match_header(tmp_path):
     """Every field offset of the ctypes mirror equals the C compiler's offsetof()."""
     import subprocess
     structs = {"flacmi_params": abi.Params, "flacmi_batch": abi.Batch,
-               "flacmi_unit_meta": abi.UnitMeta, "flacmi_outputs": abi.Outputs}
+               "flacmi_unit_meta": abi.UnitMeta, "flacmi_outputs": abi.Outputs,
+               "flacmi_frame_params": abi.FrameParams, "flacmi_decode_params": abi.DecodeParams}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
@@ -59,3 +60,33 @@ def test_create_without_device_fails_loudly():
         return
     assert not lib.flacmi_create(0)
     assert b"device" in lib.flacmi_last_error()
+
+
+def test_decode_site_and_status_codes_match_header():
+    """abi.DSITE / STATUS_* mirror enum flacmi_decode_site and the decoder status codes."""
+    text = open(HEADER).read()
+    body = text[text.index("enum flacmi_decode_site {"):]
+    body = body[:body.index("};")]
+    names = re.findall(r"FLACMI_DSITE_([A-Z0-9_]+)", body)
+    assert [n.lower() for n in names] == list(abi.DSITE)
+    assert re.search(r"FLACMI_DSITE_SYNC = 32\b", body)
+    assert int(re.search(r"#define FLACMI_STATUS_EOF (\d+)", text).group(1)) == abi.STATUS_EOF
+    assert int(re.search(r"#define FLACMI_STATUS_VERIFY (\d+)", text).group(1)) == abi.STATUS_VERIFY
+
+
+def test_decode_golden_covers_every_reference_exception_site():
+    """tests/golden/decode.json (the reference decoder's own verdicts) holds one malformed
+    frame per decoder assertion / exception and valid frames of every subframe type."""
+    import json
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "decode.json")))["cases"]
+    sites = {c["site"] for c in g if c["site"]}
+    ref_sites = [n for n in abi.DSITE if abi.DSITE[n] < abi.DSITE["crc8"]]
+    assert sorted(sites) == sorted(ref_sites)
+    for c in g:
+        assert (c["exception"] is None) == (c["site"] is None), c["name"]
+        if c["exception"]:
+            assert c["exception"] in {e.__name__ for e in abi.STATUS_EXCEPTION.values()}
+    names = {c["name"] for c in g if c["exception"] is None}
+    for must in ("constant_192", "verbatim_256", "fixed2_wasted2", "lpc32_p15", "stereo_M_S",
+                 "lpc6_rice5_escape_bs16", "fixed3_32bit"):
+        assert must in names
