@@ -143,6 +143,32 @@ def frame_writer_leg(args, cfg, az, samples, meta, rparams, residual, pstride, u
            "frames_with_status": bad_status,
            "note": "k_frame_sizes + 3-kernel scan + k_pack per call; reads the zig-zag residual rows, writes "
                    "byte-exact FLAC frames (headers, Rice codes, CRC-8/16)"}
+    # decoder round trip (BASELINE config 5): every frame decoded on the
+    # device and compared in-kernel with the source units (CRC-8/16, frame numbers and
+    # frame ends verified too)
+    dst = torch.empty(nf, dtype=torch.int32, device=dev)
+    dmm = torch.empty(nf, dtype=torch.int64, device=dev)
+    dp = abi.DecodeParams()
+    dp.channels, dp.sample_size, dp.first_frame, dp.check_crc = C, bits, 0, 1
+    eb = device_batch(samples.data_ptr(), sbytes, bits, samples.shape[1], nf * C, n)
+
+    def dcall():
+        az.decode_frames_device(out.data_ptr(), total, off.data_ptr(), nf, dp, eb, 0, 0, dst.data_ptr(),
+                                dmm.data_ptr(), sptr)
+
+    dcall()
+    torch.cuda.synchronize(dev)
+    e0.record()
+    for _ in range(2):
+        dcall()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    dms = e0.elapsed_time(e1) / 2
+    res["decoder_round_trip"] = {
+        "ms_per_call": dms, "samples_per_s": nf * C * n / (dms * 1e-3),
+        "frames_with_status": int((dst != 0).sum().item()), "samples_mismatched": int(dmm.sum().item()),
+        "note": "k_decode (one lane per frame) over every written frame, decoded samples compared in-kernel "
+                "with the source units; CRC-8/16, frame numbers and frame ends verified"}
     if check:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import frame_writer as FW  # checker only

@@ -29,7 +29,7 @@ from .common import (
 from .crc import crc8
 from .utils import batch
 
-__all__ = ["EncoderParameters", "encode", "encode_subframe_fixed", "encode_subframe_lpc",
+__all__ = ["EncoderParameters", "encode", "encode_planar", "encode_subframe_fixed", "encode_subframe_lpc",
            "encode_residual", "put_frame_header", "put_metadata_block_header",
            "put_metadata_block_streaminfo"]
 
@@ -185,13 +185,7 @@ def encode(sample_rate: int, sample_size: int, channels: int, frames: int,
     has no such mode (its -l 0 raises ValueError, which the default mode reproduces)."""
     if sample_rate <= 48_000:
         assert parameters.lpc_order.stop <= 13
-    yield MAGIC
-    yield put_metadata_block_header(
-        MetadataBlockHeader(last=True, type=MetadataBlockType.Streaminfo, length=34)).buffer
-    yield put_metadata_block_streaminfo(Streaminfo(
-        min_block_size=parameters.block_size, max_block_size=parameters.block_size,
-        min_frame_size=0, max_frame_size=0, sample_rate=sample_rate, channels=channels,
-        sample_size=sample_size, samples=frames, md5=bytes(16))).buffer
+    yield from _stream_header(sample_rate, sample_size, channels, frames, parameters)
     rmin, rmax = _rice_range(parameters.rice_partition_order)
     L = parameters.lpc_order.stop - 1
     mode = abi.MODE_FIXED_ONLY if fixed_only else abi.MODE_REFERENCE
@@ -209,6 +203,46 @@ def encode(sample_rate: int, sample_size: int, channels: int, frames: int,
         pending = []
     if pending:
         yield from _encode_batch(az, pending, index, channels, sample_size, parameters, params)
+
+
+def encode_planar(sample_rate: int, sample_size: int, pcm: np.ndarray, parameters: EncoderParameters, *,
+                  frames: Optional[int] = None, device: int = 0, blocks_per_batch: int = 8192,
+                  fixed_only: bool = False) -> Iterator[bytes]:
+    """encode() over planar PCM (int [channels][frames], e.g. from ingest.read_wav): the
+    same bytes as encode(sample_rate, sample_size, channels, frames, <the frames of pcm>,
+    parameters), without building a Python list per frame.  Blocks go to the device in
+    batches of blocks_per_batch (ingest.planar_blocks)."""
+    from .ingest import planar_blocks
+    channels, total = pcm.shape
+    if sample_rate <= 48_000:
+        assert parameters.lpc_order.stop <= 13
+    yield from _stream_header(sample_rate, sample_size, channels, total if frames is None else frames,
+                              parameters)
+    rmin, rmax = _rice_range(parameters.rice_partition_order)
+    mode = abi.MODE_FIXED_ONLY if fixed_only else abi.MODE_REFERENCE
+    params = make_params(parameters.lpc_order.stop - 1, parameters.qlp_precision, rmin, rmax, mode)
+    az = _analyzer(device)
+    n = parameters.block_size
+    nb = (total + n - 1) // n
+    for b0 in range(0, nb, blocks_per_batch):
+        rows, bits, tail_len, n_tail = planar_blocks(pcm, n, b0, blocks_per_batch)
+        data, offsets, status = az.encode_frames(rows, params, n, tail_len, n_tail, sample_bits=bits,
+                                                 channels=channels, sample_size=sample_size, first_frame=b0)
+        buf = data.tobytes()
+        for b in range(rows.shape[0] // channels):
+            st = int(status[b])
+            _raise_status(st & 0xFFFF, st >> 16)
+            yield buf[int(offsets[b]):int(offsets[b + 1])]
+
+
+def _stream_header(sample_rate, sample_size, channels, frames, parameters):
+    yield MAGIC
+    yield put_metadata_block_header(
+        MetadataBlockHeader(last=True, type=MetadataBlockType.Streaminfo, length=34)).buffer
+    yield put_metadata_block_streaminfo(Streaminfo(
+        min_block_size=parameters.block_size, max_block_size=parameters.block_size,
+        min_frame_size=0, max_frame_size=0, sample_rate=sample_rate, channels=channels,
+        sample_size=sample_size, samples=frames, md5=bytes(16))).buffer
 
 
 def _encode_batch(az, blocks, index0, channels, sample_size, parameters, params):
