@@ -75,6 +75,7 @@ struct FrameArgs {
     int64_t capacity;
     const uint16_t* crc_slice; /* [4][256] CRC-16 slice-by-4 tables */
     const uint16_t* crc_pow;   /* [28][512] multiply-by-x^(8*2^b) tables */
+    int32_t pack_split;        /* 1: k_pack32 writes the frames it can hold, k_pack the rest */
 };
 
 /* Decoder verifier (k_decode.hip): frame f = bytes [offsets[f], offsets[f+1]) of words. */

@@ -31,6 +31,8 @@
  * window words hold bits MSB first; stores byte-swap them. */
 #include "device_common.h"
 
+#include <cstdlib>
+
 namespace flacmi {
 
 constexpr int kWinWords = 4096;           /* 16 KB LDS window */
@@ -313,6 +315,21 @@ __device__ void win_flush(const FrameArgs& a, uint32_t* win, const uint16_t* ct,
     __syncthreads();
 }
 
+/* k_pack32 takes a frame when it fits one LDS window (with its alignment offset and the
+ * CRC) and every partition holds at least 8 values (a chunk of 8 meets at most one
+ * partition boundary); the launch guarantees 32-bit residuals and <= kMaxC chunks per
+ * thread. */
+constexpr int kMaxC = 4;
+__device__ __forceinline__ bool pack32_frame_ok(const FrameArgs& a, int64_t f) {
+    const int64_t bytes = a.offsets[f + 1] - a.offsets[f];
+    if (bytes + 8 > 4LL * kWinWords) return false;
+    for (int c = 0; c < a.channels; ++c) {
+        const int64_t u = f * a.channels + c;
+        if ((unit_len(a, u) >> a.meta[u].part_order) < 8) return false;
+    }
+    return true;
+}
+
 template <typename ZT>
 __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
     __shared__ uint32_t win[kWinWords];
@@ -329,6 +346,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
         return;
     }
     if (a.status[f] != 0) return;
+    if (a.pack_split && pack32_frame_ok(a, f)) return; /* written by k_pack32 */
     const int64_t F = a.offsets[f], Fend = a.offsets[f + 1];
     const int64_t u0 = f * a.channels;
     const int C = a.channels;
@@ -586,6 +604,282 @@ __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
     win_flush(a, win, ct, wb, nw, true, F, Fend, crc_acc, red);
 }
 
+/* ====================================================================================
+ * k_pack32: the frame writer for frames that fit one LDS window (32-bit residuals).
+ *
+ * One workgroup per frame.  Thread t owns a CONTIGUOUS run of 8-value chunks of each
+ * subframe (kMaxC at most, kept in registers), so one workgroup scan per subframe gives
+ * every thread the bit position of its run; the thread assembles its codes in a 64-bit
+ * register and ORs whole 32-bit words into the window (only the first and last word of a
+ * run are shared with a neighbour).  CRC-16: thread t folds a 4-byte-multiple segment of
+ * the frame ending at E - S*(NT-1-t) (E = the CRC position; window words read with a byte
+ * funnel shift, bytes before the frame treated as the leading zeros they are to a CRC that
+ * starts at 0), shifts it to E with the x^(8*2^b) tables and the workgroup XORs the
+ * shares.  The frame is stored with 16-byte stores (dword / byte stores at its two ends).
+ * ==================================================================================== */
+__global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
+    __shared__ uint32_t win[kWinWords];
+    __shared__ uint16_t ct[4 * 256];
+    __shared__ uint8_t hdr[16];
+    __shared__ uint32_t sub_start[9];
+    __shared__ int32_t cnt14[8];
+    __shared__ uint32_t red[kPackThreads / 64];
+    __shared__ int hb_s;
+    const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t f = blockIdx.x;
+    if (a.offsets[a.n_frames] > a.capacity) return; /* k_pack reports it */
+    if (a.status[f] != 0 || !pack32_frame_ok(a, f)) return;
+    const int64_t F = a.offsets[f], Fend = a.offsets[f + 1];
+    const int64_t u0 = f * a.channels;
+    const int C = a.channels;
+    const uint32_t A = (uint32_t)(8 * (F & 3)); /* aligned bit of the frame's first bit */
+    const int nwf = (int)(((F & 3) + (Fend - F) + 3) >> 2); /* window words of the frame */
+    for (int i = tid; i < 4 * 256; i += NT) ct[i] = a.crc_slice[i];
+    for (int i = tid; i < nwf; i += NT) win[i] = 0;
+    if (tid < 8) cnt14[tid] = 0;
+    if (tid == 0) hb_s = frame_header(a.first_frame + f, unit_len(a, u0), hdr);
+    __syncthreads();
+    for (int c = 0; c < C; ++c) {
+        const flacmi_unit_meta& m = a.meta[u0 + c];
+        if (m.coding_method == 5) {
+            const int32_t* rp = a.rice_params + (u0 + c) * a.params_stride;
+            int cnt = 0;
+            for (int k = tid; k < m.n_parts; k += NT) cnt += rp[k] > 14 ? 1 : 0;
+            if (cnt) atomicAdd(&cnt14[c], cnt);
+        }
+    }
+    __syncthreads();
+    const int hb = hb_s;
+    if (tid == 0) {
+        uint32_t s = A + 8u * (uint32_t)hb;
+        for (int c = 0; c < C; ++c) {
+            const flacmi_unit_meta& m = a.meta[u0 + c];
+            sub_start[c] = s;
+            s += sub_prefix_bits(m, a.sample_size, a.q) + (uint32_t)sub_residual_bits(m, cnt14[c]);
+        }
+        sub_start[C] = s;
+    }
+    if (tid < hb) win_or(win, 0, A + 8u * tid, hdr[tid], 8);
+    __syncthreads();
+
+    const int ss = a.sample_size, q = a.q;
+    for (int c = 0; c < C; ++c) {
+        const int64_t u = u0 + c;
+        const flacmi_unit_meta& m = a.meta[u];
+        const int n = unit_len(a, u);
+        const int order = m.order, ncoefs = m.ncoefs, method = m.coding_method;
+        const bool lpc = m.kind == FLACMI_KIND_LPC;
+        const uint32_t s0 = sub_start[c];
+        const uint32_t pre = sub_prefix_bits(m, ss, q);
+        /* subframe header, warm-up, LPC fields, residual header: field t per thread */
+        const int nfields = 1 + order + (lpc ? 2 + ncoefs : 0) + 2;
+        for (int t = tid; t < nfields; t += NT) {
+            uint32_t pos;
+            uint64_t v;
+            int w;
+            const uint32_t b = s0 + 8 + (uint32_t)order * ss;
+            const int t2 = t - 1 - order;
+            if (t == 0) {
+                pos = s0;
+                v = lpc ? (uint64_t)((0x20 | (order - 1)) << 1) : (uint64_t)((0x08 | order) << 1);
+                w = 8;
+            } else if (t <= order) {
+                const int j = t - 1;
+                const int64_t x = a.sample_bytes == 2 ? (int64_t)((const int16_t*)a.samples)[u * a.stride + j]
+                                                      : (int64_t)((const int32_t*)a.samples)[u * a.stride + j];
+                pos = s0 + 8 + (uint32_t)j * ss;
+                v = (uint64_t)x & (ss == 64 ? ~0ull : ((1ull << ss) - 1));
+                w = ss;
+            } else if (lpc && t2 == 0) {
+                pos = b;
+                v = (uint64_t)((q - 1) & 15);
+                w = 4;
+            } else if (lpc && t2 == 1) {
+                pos = b + 4;
+                v = (uint64_t)(m.shift & 31);
+                w = 5;
+            } else if (lpc && t2 < 2 + ncoefs) {
+                const int j = t2 - 2;
+                pos = b + 9 + (uint32_t)j * q;
+                v = (uint64_t)(int64_t)m.coefs[j] & ((1ull << q) - 1);
+                w = q;
+            } else {
+                const int t3 = t2 - (lpc ? 2 + ncoefs : 0);
+                const uint32_t b2 = b + (lpc ? 9u + (uint32_t)ncoefs * q : 0u);
+                pos = t3 == 0 ? b2 : b2 + 2;
+                v = t3 == 0 ? (method == 5 ? 1 : 0) : (uint64_t)(m.part_order & 15);
+                w = t3 == 0 ? 2 : 4;
+            }
+            win_or(win, 0, pos, v, w);
+        }
+        /* residual: this thread's chunks [k0, k1) */
+        const int ps = n >> m.part_order;
+        const int32_t* __restrict__ rp = a.rice_params + u * a.params_stride;
+        const uint32_t* __restrict__ zrow = reinterpret_cast<const uint32_t*>(a.residual) + u * a.residual_stride;
+        const int nch = (n + 7) >> 3;
+        const int cpt = (nch + NT - 1) / NT;
+        const int k0 = tid * cpt, k1 = min(k0 + cpt, nch);
+        uint32_t z[kMaxC][8];
+        int pa[kMaxC], pb[kMaxC], bnd[kMaxC];
+        uint32_t tsum = 0;
+#pragma unroll
+        for (int j = 0; j < kMaxC; ++j) {
+            const int k = k0 + j;
+            const int i0 = 8 * k;
+            pa[j] = pb[j] = 0;
+            bnd[j] = 1 << 30;
+            if (k < k1) {
+                const uint4 v0 = *reinterpret_cast<const uint4*>(zrow + i0);
+                const uint4 v1 = *reinterpret_cast<const uint4*>(zrow + i0 + 4);
+                z[j][0] = v0.x; z[j][1] = v0.y; z[j][2] = v0.z; z[j][3] = v0.w;
+                z[j][4] = v1.x; z[j][5] = v1.y; z[j][6] = v1.z; z[j][7] = v1.w;
+                const int part0 = i0 / ps;
+                const int b1 = (part0 + 1) * ps;
+                pa[j] = rp[part0];
+                pb[j] = (b1 < n && b1 <= i0 + 7) ? rp[part0 + 1] : pa[j];
+                bnd[j] = b1;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int i = i0 + e;
+                    const int p = i >= b1 ? pb[j] : pa[j];
+                    const bool valid = i >= order && i < n;
+                    const bool first = i == order || (i > order && (i == b1 || i == part0 * ps));
+                    tsum += valid ? (first ? (uint32_t)method : 0u) + (z[j][e] >> p) + 1u + (uint32_t)p : 0u;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) z[j][e] = 0;
+            }
+        }
+        /* workgroup exclusive scan of tsum */
+        uint32_t v = tsum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)v, o);
+            if (lane >= o) v += t;
+        }
+        if (lane == 63) red[wid] = v;
+        __syncthreads();
+        uint32_t pre_w = 0;
+        for (int w2 = 0; w2 < wid; ++w2) pre_w += red[w2];
+        uint32_t pos = s0 + pre + pre_w + v - tsum;
+        uint32_t widx = pos >> 5;
+        uint64_t acc = 0;
+        auto emit = [&](uint32_t wi, uint32_t val) __attribute__((always_inline)) {
+            if (val != 0) atomicOr(&win[wi], val);
+        };
+        /* val right-aligned, 1 <= w <= 32; keeps pos - 32*widx in [0, 32) */
+        auto put = [&](uint32_t val, int w) __attribute__((always_inline)) {
+            const int off = (int)(pos - 32u * widx);
+            acc |= (uint64_t)val << (64 - off - w);
+            pos += (uint32_t)w;
+            if (pos - 32u * widx >= 32u) {
+                emit(widx, (uint32_t)(acc >> 32));
+                acc <<= 32;
+                ++widx;
+            }
+        };
+        const uint32_t pmask_m = (1u << method) - 1u;
+#pragma unroll
+        for (int j = 0; j < kMaxC; ++j) {
+            const int k = k0 + j;
+            if (k < k1) {
+                const int i0 = 8 * k;
+                const int part0 = i0 / ps;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int i = i0 + e;
+                    if (i >= order && i < n) {
+                        const int p = i >= bnd[j] ? pb[j] : pa[j];
+                        const bool first = i == order || (i > order && (i == bnd[j] || i == part0 * ps));
+                        if (first) put((uint32_t)p & pmask_m, method);
+                        const uint32_t zk = z[j][e];
+                        const uint32_t qv = zk >> p;
+                        if (qv != 0) { /* unary zeros */
+                            pos += qv;
+                            if (pos - 32u * widx >= 32u) {
+                                emit(widx, (uint32_t)(acc >> 32));
+                                acc = 0;
+                                widx = pos >> 5;
+                            }
+                        }
+                        put((1u << p) | (zk & ((1u << p) - 1u)), p + 1); /* p <= 30 for narrow values */
+                    }
+                }
+            }
+        }
+        if (pos != 32u * widx) emit(widx, (uint32_t)(acc >> 32));
+        __syncthreads(); /* red[] reuse by the next subframe's scan */
+    }
+
+    /* CRC-16 of bytes [F, E), E = Fend - 2.  Window byte r is frame byte F - (F & 3) + r. */
+    const int64_t E = Fend - 2;
+    const int64_t Fa = F & ~3LL;
+    const int64_t seg = (((E - F) + NT - 1) / NT + 3) & ~3LL; /* bytes per thread, multiple of 4 */
+    {
+        const int64_t b1 = E - seg * (NT - 1 - tid);
+        const int64_t b0 = b1 - seg;
+        uint32_t crc = 0;
+        if (b1 > F) {
+            const int64_t r0 = b0 - Fa; /* may be negative: those bytes precede the frame */
+            const int o = (int)(((E - Fa) & 3));
+            for (int64_t r = r0; r < b1 - Fa; r += 4) {
+                uint32_t w;
+                if (r + 4 <= 0) continue; /* wholly before the window */
+                const int64_t k = r >> 2; /* floor: r may be -1..-3 only when o != 0 */
+                const uint32_t lo = k >= 0 ? win[k] : 0u;
+                const uint32_t hi = (k + 1) < nwf ? win[k + 1] : 0u;
+                w = o ? ((lo << (8 * o)) | (hi >> (32 - 8 * o))) : lo;
+                /* bytes before F are zero in the window already (the frame's first word is
+                 * shared only in the output, not in this window) */
+                crc = (uint32_t)ct[3 * 256 + ((crc >> 8) ^ (w >> 24))] ^ (uint32_t)ct[2 * 256 + ((crc ^ (w >> 16)) & 0xFF)] ^
+                      (uint32_t)ct[256 + ((w >> 8) & 0xFF)] ^ (uint32_t)ct[w & 0xFF];
+            }
+            crc = crc16_mulpow(crc, E - b1, a.crc_pow);
+        }
+        for (int o2 = 32; o2 >= 1; o2 >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o2);
+        if (lane == 0) red[wid] = crc;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t x = 0;
+            for (int w2 = 0; w2 < NT / 64; ++w2) x ^= red[w2];
+            win_or(win, 0, (uint32_t)(8 * (F & 3) + 8 * (E - F)), x & 0xFFFF, 16);
+        }
+        __syncthreads();
+    }
+
+    /* store: window word k is output word (F >> 2) + k */
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(a.out);
+    const int64_t g0 = F >> 2;
+    const int64_t gf = (F + 3) >> 2;   /* first word wholly inside the frame */
+    const int64_t ge = Fend >> 2;      /* words [gf, ge) are wholly inside */
+    if (tid < 4) { /* partial words at both ends: byte stores */
+        const int64_t g = tid < 2 ? g0 : ge;
+        const int j = tid & 1 ? 2 : 0;
+        for (int jj = j; jj < j + 2; ++jj) {
+            const int64_t B = 4 * g + jj;
+            if (B >= F && B < Fend && !(g >= gf && g < ge)) a.out[B] = (uint8_t)(win[g - g0] >> (24 - 8 * jj));
+        }
+    }
+    if (gf < ge) {
+        const int64_t mis = (int64_t)(((uintptr_t)a.out >> 2) & 3); /* out is 4-byte aligned */
+        const int64_t ga = ((gf + mis + 3) & ~3LL) - mis; /* 16-byte aligned output words [ga, gz) */
+        const int64_t gz = ((ge + mis) & ~3LL) - mis;
+        if (ga < gz) {
+            for (int64_t g = ga + 4 * tid; g < gz; g += 4 * NT) {
+                const int64_t k = g - g0;
+                uint4 v{__builtin_bswap32(win[k]), __builtin_bswap32(win[k + 1]), __builtin_bswap32(win[k + 2]),
+                        __builtin_bswap32(win[k + 3])};
+                *reinterpret_cast<uint4*>(out32 + g) = v;
+            }
+            if (tid < 3 && gf + tid < ga) out32[gf + tid] = __builtin_bswap32(win[gf + tid - g0]);
+            if (tid >= 4 && tid < 7 && gz + (tid - 4) < ge) out32[gz + tid - 4] = __builtin_bswap32(win[gz + tid - 4 - g0]);
+        } else if (tid < 4) {
+            for (int64_t g = gf + tid; g < ge; g += 4) out32[g] = __builtin_bswap32(win[g - g0]);
+        }
+    }
+}
+
 hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s) {
     if (a.n_frames <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_frame_sizes, dim3((unsigned)((a.n_frames + 3) / 4)), dim3(256), 0, s, a);
@@ -608,10 +902,18 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     const int tiles = (nch + kPackThreads - 1) / kPackThreads;
     int nt = 64 * ((nch + 64 * tiles - 1) / (64 * tiles));
     nt = nt < 64 ? 64 : nt;
-    if (a.residual_bytes == 8)
+    if (a.residual_bytes == 8) {
         hipLaunchKernelGGL(k_pack<uint64_t>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_pack<uint32_t>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, a);
+        return hipGetLastError();
+    }
+    FrameArgs b = a;
+    b.pack_split = (tiles == 1 || (nch + nt - 1) / nt <= kMaxC) && getenv("FLACMI_NO_PACK32") == nullptr;
+    if (b.pack_split) {
+        hipLaunchKernelGGL(k_pack32, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_pack<uint32_t>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
     return hipGetLastError();
 }
 
