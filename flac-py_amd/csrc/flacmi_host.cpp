@@ -158,7 +158,7 @@ struct flacmi_ctx {
     std::map<int, std::pair<int, int>> window_one; /* per n: [lo, hi) where the weight is 1.0 */
     DevBuf rec, retry, h_samples, h_meta, h_params, h_residual, h_acf, h_fs, h_ls, h_recs;
     uint16_t* d_crc = nullptr;  /* CRC-16 slice tables [4][256] + power tables [28][512] */
-    DevBuf scan, h_offsets, h_status, h_frames, dec;
+    DevBuf scan, h_offsets, h_status, h_frames, dec, slow;
     int64_t frames_bytes = 0;   /* bytes of the last flacmi_encode_host call */
     static constexpr int kRing = 64;
     static constexpr int kMaxChunks = 8;
@@ -246,7 +246,7 @@ void flacmi_destroy(flacmi_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
     for (auto& kv : ctx->windows) (void)hipFree(kv.second);
-    for (DevBuf* b : {&ctx->dec, &ctx->rec, &ctx->retry, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
+    for (DevBuf* b : {&ctx->slow, &ctx->dec, &ctx->rec, &ctx->retry, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
                       &ctx->h_fs, &ctx->h_ls, &ctx->h_recs, &ctx->scan, &ctx->h_offsets, &ctx->h_status,
                       &ctx->h_frames})
         if (b->p) (void)hipFree(b->p);
@@ -641,6 +641,14 @@ static FrameArgs frame_args(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi
     return a;
 }
 
+/* the k_pack32 -> k_pack hand-off list (count word + one index per frame) */
+static int pack_lists(flacmi_ctx* ctx, FrameArgs& a) {
+    if (int rc = ensure_buf(ctx->slow, sizeof(int64_t) * (size_t)(a.n_frames + 2))) return rc;
+    a.slow_count = (unsigned long long*)ctx->slow.p;
+    a.slow_list = (int64_t*)ctx->slow.p + 2;
+    return 0;
+}
+
 static int frame_sizes_impl(flacmi_ctx* ctx, FrameArgs& a, int64_t* offsets, int32_t* status, hipStream_t s) {
     a.offsets = offsets;
     a.status = status;
@@ -690,6 +698,7 @@ int flacmi_pack_frames_device(flacmi_ctx* ctx, const flacmi_batch* batch, const 
     a.status = frame_status;
     a.out = out;
     a.capacity = out_capacity;
+    if (int rc = pack_lists(ctx, a)) return rc;
     HIP_TRY(launch_pack(a, (hipStream_t)stream));
     return 0;
 }
@@ -804,6 +813,7 @@ int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_
         a.status = (int32_t*)ctx->h_status.p;
         a.out = (uint8_t*)ctx->h_frames.p;
         a.capacity = total;
+        if (int rc = pack_lists(ctx, a)) return rc;
         HIP_TRY(launch_pack(a, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         ctx->frames_bytes = total;

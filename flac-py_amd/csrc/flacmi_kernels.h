@@ -76,6 +76,10 @@ struct FrameArgs {
     const uint16_t* crc_slice; /* [4][256] CRC-16 slice-by-4 tables */
     const uint16_t* crc_pow;   /* [28][512] multiply-by-x^(8*2^b) tables */
     int32_t pack_split;        /* 1: k_pack32 writes the frames it can hold, k_pack the rest */
+    unsigned long long* slow_count; /* pack_split: frames k_pack32 hands to k_pack: count, */
+    int64_t* slow_list;              /* and their indices ([n_frames]) */
+    int32_t ablate;            /* profiling only (env FLACMI_PACK_ABLATE): 1 no CRC shift, 2 no residual codes,
+                                  3 neither (output invalid) */
 };
 
 /* Decoder verifier (k_decode.hip): frame f = bytes [offsets[f], offsets[f+1]) of words. */

@@ -331,7 +331,7 @@ __device__ __forceinline__ bool pack32_frame_ok(const FrameArgs& a, int64_t f) {
 }
 
 template <typename ZT>
-__global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
+__device__ __forceinline__ void pack_frame(const FrameArgs& a, const int64_t f) {
     __shared__ uint32_t win[kWinWords];
     __shared__ uint16_t ct[4 * 256];
     __shared__ uint8_t hdr[16];
@@ -340,13 +340,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
     __shared__ uint32_t red[8];
     __shared__ int hb_s;
     const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, wid = tid >> 6;
-    const int64_t f = blockIdx.x;
-    if (a.offsets[a.n_frames] > a.capacity) {
-        if (f == 0 && tid == 0) a.status[0] = (FLACMI_SITE_FRAME_SIZE << 16) | FLACMI_STATUS_FRAME_TOO_LARGE;
-        return;
-    }
     if (a.status[f] != 0) return;
-    if (a.pack_split && pack32_frame_ok(a, f)) return; /* written by k_pack32 */
     const int64_t F = a.offsets[f], Fend = a.offsets[f + 1];
     const int64_t u0 = f * a.channels;
     const int C = a.channels;
@@ -604,6 +598,22 @@ __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
     win_flush(a, win, ct, wb, nw, true, F, Fend, crc_acc, red);
 }
 
+/* General frame writer: every frame (pack_split = 0), or, after k_pack32, the frames it
+ * listed (grid-stride over the list; an empty list costs one short launch). */
+template <typename ZT>
+__global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
+    if (a.offsets[a.n_frames] > a.capacity) {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            a.status[0] = (FLACMI_SITE_FRAME_SIZE << 16) | FLACMI_STATUS_FRAME_TOO_LARGE;
+        return;
+    }
+    const int64_t cnt = a.pack_split ? (int64_t)*a.slow_count : (int64_t)blockIdx.x + 1;
+    for (int64_t idx = blockIdx.x; idx < cnt; idx += gridDim.x) { /* one call site: inlined once */
+        pack_frame<ZT>(a, a.pack_split ? a.slow_list[idx] : idx);
+        __syncthreads(); /* LDS reuse by the next frame */
+    }
+}
+
 /* ====================================================================================
  * k_pack32: the frame writer for frames that fit one LDS window (32-bit residuals).
  *
@@ -628,7 +638,11 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
     const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, wid = tid >> 6;
     const int64_t f = blockIdx.x;
     if (a.offsets[a.n_frames] > a.capacity) return; /* k_pack reports it */
-    if (a.status[f] != 0 || !pack32_frame_ok(a, f)) return;
+    if (a.status[f] != 0) return;
+    if (!pack32_frame_ok(a, f)) { /* k_pack writes it */
+        if (threadIdx.x == 0) a.slow_list[atomicAdd(a.slow_count, 1ull)] = f;
+        return;
+    }
     const int64_t F = a.offsets[f], Fend = a.offsets[f + 1];
     const int64_t u0 = f * a.channels;
     const int C = a.channels;
@@ -720,7 +734,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
         const int cpt = (nch + NT - 1) / NT;
         const int k0 = tid * cpt, k1 = min(k0 + cpt, nch);
         uint32_t z[kMaxC][8];
-        int pa[kMaxC], pb[kMaxC], bnd[kMaxC];
+        int pa[kMaxC], pb[kMaxC], bnd[kMaxC], pt0[kMaxC];
         uint32_t tsum = 0;
 #pragma unroll
         for (int j = 0; j < kMaxC; ++j) {
@@ -734,6 +748,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
                 z[j][0] = v0.x; z[j][1] = v0.y; z[j][2] = v0.z; z[j][3] = v0.w;
                 z[j][4] = v1.x; z[j][5] = v1.y; z[j][6] = v1.z; z[j][7] = v1.w;
                 const int part0 = i0 / ps;
+                pt0[j] = part0;
                 const int b1 = (part0 + 1) * ps;
                 pa[j] = rp[part0];
                 pb[j] = (b1 < n && b1 <= i0 + 7) ? rp[part0 + 1] : pa[j];
@@ -783,27 +798,39 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
 #pragma unroll
         for (int j = 0; j < kMaxC; ++j) {
             const int k = k0 + j;
-            if (k < k1) {
+            if (k < k1 && !(a.ablate & 2)) {
                 const int i0 = 8 * k;
-                const int part0 = i0 / ps;
+                const int part0 = pt0[j];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     const int i = i0 + e;
                     if (i >= order && i < n) {
                         const int p = i >= bnd[j] ? pb[j] : pa[j];
                         const bool first = i == order || (i > order && (i == bnd[j] || i == part0 * ps));
-                        if (first) put((uint32_t)p & pmask_m, method);
                         const uint32_t zk = z[j][e];
                         const uint32_t qv = zk >> p;
-                        if (qv != 0) { /* unary zeros */
+                        const uint32_t code = (1u << p) | (zk & ((1u << p) - 1u)); /* p <= 30: narrow values */
+                        /* usually the parameter, the q zeros and the code fit one put of <= 32 bits */
+                        uint32_t val = code, w = qv + 1u + (uint32_t)p;
+                        if (first) {
+                            if (w + (uint32_t)method <= 32u) {
+                                val |= ((uint32_t)p & pmask_m) << w;
+                                w += (uint32_t)method;
+                            } else {
+                                put((uint32_t)p & pmask_m, method);
+                            }
+                        }
+                        if (w <= 32u) {
+                            put(val, (int)w);
+                        } else { /* long unary run */
                             pos += qv;
                             if (pos - 32u * widx >= 32u) {
                                 emit(widx, (uint32_t)(acc >> 32));
                                 acc = 0;
                                 widx = pos >> 5;
                             }
+                            put(code, p + 1);
                         }
-                        put((1u << p) | (zk & ((1u << p) - 1u)), p + 1); /* p <= 30 for narrow values */
                     }
                 }
             }
@@ -835,7 +862,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
                 crc = (uint32_t)ct[3 * 256 + ((crc >> 8) ^ (w >> 24))] ^ (uint32_t)ct[2 * 256 + ((crc ^ (w >> 16)) & 0xFF)] ^
                       (uint32_t)ct[256 + ((w >> 8) & 0xFF)] ^ (uint32_t)ct[w & 0xFF];
             }
-            crc = crc16_mulpow(crc, E - b1, a.crc_pow);
+            if (!(a.ablate & 1)) crc = crc16_mulpow(crc, E - b1, a.crc_pow);
         }
         for (int o2 = 32; o2 >= 1; o2 >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o2);
         if (lane == 0) red[wid] = crc;
@@ -908,12 +935,17 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     }
     FrameArgs b = a;
     b.pack_split = (tiles == 1 || (nch + nt - 1) / nt <= kMaxC) && getenv("FLACMI_NO_PACK32") == nullptr;
+    const char* ab = getenv("FLACMI_PACK_ABLATE");
+    b.ablate = ab ? atoi(ab) : 0;
     if (b.pack_split) {
+        hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
+        if (e0 != hipSuccess) return e0;
         hipLaunchKernelGGL(k_pack32, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_pack<uint32_t>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
+    const int64_t grid = b.pack_split ? (a.n_frames < 4096 ? a.n_frames : 4096) : a.n_frames;
+    hipLaunchKernelGGL(k_pack<uint32_t>, dim3((unsigned)grid), dim3(nt), 0, s, b);
     return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@ def rows(pattern):
     return out
 
 
-STAGES = ("k_resid", "k_lpc", "k_stats", "k_synth", "k_pack", "k_frame_sizes", "k_decode")
+STAGES = ("k_resid", "k_lpc", "k_stats", "k_synth", "k_pack32", "k_pack", "k_frame_sizes", "k_decode", "k_decorr")
 
 
 def short(name):
