@@ -27,6 +27,12 @@ CONFIGS = {
     # configs[2]: stereo 24-bit/96 kHz, -b 16384 -l 32 -q 15 -r 0,8 (each channel one unit)
     "c3": dict(workload="stereo 24-bit 16384-sample blocks, -l 32 -q 15 -r 0,8",
                n=16384, bits=24, L=32, q=15, rmin=0, rmax=8, mode=0, units=100_000, channels=2),
+    # configs[3]: 1e8 blocks of config 2's shape, generated on the device chunk by chunk
+    # (9.2e11 bytes of PCM cannot be materialised); chunks go round-robin to the ranks and
+    # one step is the whole 1e8 blocks: strong scaling, generation inside the timed region
+    "c4": dict(workload="1e8 synthetic mono 4608-sample int16 blocks generated on device in 1e6-block chunks, "
+                        "-l 12 -q 5 -r 0,5", n=4608, bits=16, L=12, q=5, rmin=0, rmax=5, mode=0,
+               units=1_000_000, channels=1, total_units=100_000_000),
     # configs[4]: fixed-only (-l 0 mode of this build) + Rice search
     "c5": dict(workload="fixed-only 4608-sample int16 blocks, -r 0,5",
                n=4608, bits=16, L=0, q=5, rmin=0, rmax=5, mode=1, units=1_000_000, channels=1),
@@ -41,7 +47,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--units", type=int, default=0, help="units per GPU (default: the config's)")
+    ap.add_argument("--units", type=int, default=0, help="units per GPU (default: the config's); c4: chunk size")
+    ap.add_argument("--total-units", type=int, default=0, help="c4: blocks in the whole job (default 1e8)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--parity-units", type=int, default=64)
@@ -258,11 +265,29 @@ def main():
     az.synth_device(samples.data_ptr(), sbytes, bits, sstride, first_unit, units, n, args.seed, sptr)
     params = make_params(cfg["L"], cfg["q"], cfg["rmin"], cfg["rmax"], cfg["mode"])
 
+    chunked = "total_units" in cfg
+    total_units = (args.total_units or cfg["total_units"]) if chunked else world * units
+    n_chunks = (total_units + units - 1) // units
+    my_chunks = list(range(rank, n_chunks, world)) if chunked else []
+    stats_acc = torch.zeros_like(stats)
+
     def step():
-        az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, units, n, params, meta.data_ptr(),
-                          rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, sptr)
-        az.stream_stats(meta.data_ptr(), units, n, stats.data_ptr(), sptr)
-        reduce_stats(stats, dist)
+        if not chunked:
+            az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, units, n, params, meta.data_ptr(),
+                              rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, sptr)
+            az.stream_stats(meta.data_ptr(), units, n, stats.data_ptr(), sptr)
+            reduce_stats(stats, dist)
+            return
+        stats_acc.zero_()
+        for ci in my_chunks:  # round-robin chunks: generate, analyse, count
+            cu = min(units, total_units - ci * units)
+            az.synth_device(samples.data_ptr(), sbytes, bits, sstride, ci * units, cu, n, args.seed, sptr)
+            az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, cu, n, params, meta.data_ptr(),
+                              rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, sptr)
+            az.stream_stats(meta.data_ptr(), cu, n, stats.data_ptr(), sptr)
+            stats_acc.add_(stats)
+        reduce_stats(stats_acc, dist)
+        stats.copy_(stats_acc)
 
     for _ in range(args.warmup):
         step()
@@ -284,7 +309,7 @@ def main():
 
     meta_np = meta.cpu().numpy().view(abi.META_DTYPE).reshape(units)
     st = stats.cpu().numpy()
-    total_samples = world * units * n * args.steps
+    total_samples = total_units * n * args.steps
     value = total_samples / elapsed
 
     # ---- parity: sampled units vs the CPU oracle (outside the timed region) ----
@@ -313,7 +338,7 @@ def main():
                   "check": "meta, coefficients, zig-zag residual and Rice parameters bit-exact vs oracle"}
 
     frames = None
-    if not args.no_frames:
+    if not args.no_frames and not chunked:
         frames = frame_writer_leg(args, cfg, az, samples, meta, rparams, residual, pstride, units, sptr,
                                   rank == 0 and not args.no_parity)
 
@@ -342,11 +367,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if chunked else "weak",
             "vs_baseline": None,
             "dtype": "i16 in; f64 autocorrelation/Levinson; i32 predictors",
             "data": "synthetic: on-device integer generator (3 DDS tones + splitmix64 noise, SURVEY §8d)",
-            "config": {"workload": cfg["workload"], "units_per_gpu": units, "block": n, "sample_bits": bits,
+            "config": {"workload": cfg["workload"], "units_per_gpu": total_units // world,
+                       "units_total": total_units, "chunk_units": units if chunked else None, "block": n, "sample_bits": bits,
                        "max_lpc_order": cfg["L"], "qlp_precision": cfg["q"], "rice": [cfg["rmin"], cfg["rmax"]],
                        "mode": "fixed-only" if cfg["mode"] else "reference", "parallelism": f"dp{world} (block shards)"},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": dom_gbs, "peak": HBM_PEAK_GBS,

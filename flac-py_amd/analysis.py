@@ -256,7 +256,7 @@ class Analyzer:
                      first_unit: int, n_units: int, length: int, seed: int, stream: int = 0) -> None:
         done = 0
         while done < n_units:
-            k = min(65535, n_units - done)
+            k = min(1 << 30, n_units - done)
             check(self.lib.flacmi_synth_device(self.ctx, dst_ptr + done * unit_stride * sample_bytes,
                                                sample_bytes, sample_bits, unit_stride, first_unit + done,
                                                k, length, seed, stream), "flacmi_synth_device")

@@ -852,7 +852,7 @@ int flacmi_synth_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_
     if (sample_bits < 8 || sample_bits > 8 * sample_bytes || (sample_bits > 16 && sample_bits - 16 > 15))
         return fail(FLACMI_E_INVALID, "sample_bits out of range");
     if (len < 1 || unit_stride < len) return fail(FLACMI_E_INVALID, "bad length/stride");
-    if (n_units > 65535) return fail(FLACMI_E_INVALID, "at most 65535 units per synth call");
+    if (n_units > 0x7fffffff) return fail(FLACMI_E_INVALID, "at most 2^31-1 units per synth call");
     if (int rc = set_device(ctx)) return rc;
     HIP_TRY(launch_synth(dst, sample_bytes, sample_bits, unit_stride, first_unit, n_units, len, seed, ctx->d_sintab,
                          (hipStream_t)stream));

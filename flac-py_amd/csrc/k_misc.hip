@@ -40,7 +40,7 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_synth(T* dst, int32_t bits, int64_t stride, int64_t first_unit,
                                                int32_t len, uint64_t seed, const int32_t* __restrict__ sintab) {
-    const int64_t uu = blockIdx.y;
+    const int64_t uu = blockIdx.x;
     const int64_t unit = first_unit + uu;
     const uint64_t h0 = splitmix64(seed ^ ((uint64_t)unit * 0xD1B54A32D192ED03ull));
     int64_t amp[3];
@@ -55,14 +55,31 @@ __global__ __launch_bounds__(256) void k_synth(T* dst, int32_t bits, int64_t str
     }
     const int64_t sigma = 66 + (int64_t)(splitmix64(h0 + 4) % 590);
     const int64_t lo = -(1LL << (bits - 1)), hi = (1LL << (bits - 1)) - 1;
-    for (int i = blockIdx.x * 256 + threadIdx.x; i < len; i += gridDim.x * 256) {
-        int64_t acc = 0;
+    /* the 4096-entry sine table in LDS; phases advance by 256 * dphi per iteration.
+     * amp < 2^14 and |sintab| <= 2^15, so each product is an exact 24-bit multiply and
+     * the sum of three fits 32 bits: the same values as the int64 recipe. */
+    __shared__ int32_t tab[4096];
+    for (int t = threadIdx.x; t < 4096; t += 256) tab[t] = sintab[t];
+    __syncthreads();
+    uint32_t ph[3], st[3];
+    int32_t a32[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) acc += amp[k] * sintab[(uint32_t)(phi0[k] + (uint32_t)i * dphi[k]) >> 20];
-        const int64_t s = acc >> 15;
+    for (int k = 0; k < 3; ++k) {
+        ph[k] = phi0[k] + (uint32_t)threadIdx.x * dphi[k];
+        st[k] = 256u * dphi[k];
+        a32[k] = (int32_t)amp[k];
+    }
+    for (int i = threadIdx.x; i < len; i += 256) {
+        int32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            acc += __mul24(a32[k], tab[ph[k] >> 20]);
+            ph[k] += st[k];
+        }
+        const int64_t s = (int64_t)(acc >> 15);
         const uint64_t r = splitmix64(seed ^ ((uint64_t)unit << 32) ^ (uint64_t)i);
         const int64_t bsum = (int64_t)((r & 0xff) + ((r >> 8) & 0xff) + ((r >> 16) & 0xff) + ((r >> 24) & 0xff));
-        int64_t v = s + (((bsum - 510) * sigma) >> 7);
+        int64_t v = s + (int64_t)((__mul24((int32_t)(bsum - 510), (int32_t)sigma)) >> 7);
         if (bits > 16) {
             const int e = bits - 16;
             v = v * (1LL << e) + (int64_t)((r >> 32) & ((1ull << e) - 1)) - (1LL << (e - 1));
@@ -138,7 +155,9 @@ hipError_t launch_expand_records(const int32_t* rec, int32_t rec_words, int32_t 
 hipError_t launch_synth(void* dst, int32_t sample_bytes, int32_t bits, int64_t stride, int64_t first_unit,
                         int64_t n_units, int32_t len, uint64_t seed, const int32_t* sintab, hipStream_t s) {
     if (n_units <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((len + 255) / 256), (unsigned)n_units);
+    /* one workgroup per unit: the per-unit recipe (64-bit splitmix, divisions) is scalar
+     * work each wave repeats, so every thread loops over len / 256 samples */
+    const dim3 grid((unsigned)n_units);
     if (sample_bytes == 2)
         hipLaunchKernelGGL(k_synth<int16_t>, grid, dim3(256), 0, s, (int16_t*)dst, bits, stride, first_unit, len, seed, sintab);
     else
