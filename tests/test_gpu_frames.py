@@ -3,7 +3,8 @@
 tests/test_frame_writer_golden.py): every frame byte-identical, on the oracle's own
 analysis of the same units, for the BASELINE config shapes and the header / writer edge
 cases (explicit 8/16-bit block sizes, 1..6-byte coded numbers, frames larger than the
-kernel's 16 KB LDS window, Rice5Bit, frame-number overflow, the q = 16 writer assert)."""
+kernel's 16 KB LDS window, Rice5Bit, frame-number overflow, the q = 16 writer assert), and
+frames that k_pack32 hands to the general k_pack."""
 import numpy as np
 import pytest
 
@@ -34,6 +35,8 @@ CASES = {
     "q16_assert": (12, 1, 1152, 0, 16, 8, 16, 0, 4, 0, 16, 0, 18),
     "overflow": (6, 1, 576, 0, 16, 4, 5, 0, 3, 0, 16, (1 << 31) - 3, 19),
     "wide20": (6, 2, 4096, 0, 20, 12, 14, 0, 6, 0, 20, 9, 20),
+    # frames > the 16 KB LDS window while k_pack32 is active: handed to k_pack by list
+    "big3ch_list": (8, 3, 4608, 0, 20, 12, 12, 0, 5, 0, 20, 3, 21),
 }
 
 
@@ -68,6 +71,8 @@ def test_frames_match_oracle_writer(az, name):
                          f"{next((i for i in range(min(len(got), len(w))) if got[i] != w[i]), None)}"
     if name == "overflow":
         assert [int(s) >> 16 for s in status] == [0, 0, 0, 15, 15, 15]
+    if name == "big3ch_list":
+        assert (np.diff(offsets) + 8 > 4 * 4096).all()  # every frame takes the k_pack hand-off
     if name in ("c3_stereo", "c3_tail"):
         full = np.diff(offsets)[: frames - (1 if tail else 0)]
         assert (full > 4 * 4096).all()  # every full frame spans several 16 KB LDS windows
@@ -111,3 +116,18 @@ def test_device_pointer_path_matches_host_path(az):
     torch.cuda.synchronize(dev)
     assert int(st[0].item()) == (17 << 16) | abi.STATUS_FRAME_TOO_LARGE
     assert not small.cpu().numpy().any()
+
+
+@pytest.mark.parametrize("name", ["c2", "c1_tail", "bs16_3ch"])
+def test_general_writer_alone_matches(az, name, monkeypatch):
+    """FLACMI_NO_PACK32=1: every frame through the general k_pack gives the same bytes."""
+    frames, C, n, tail, bits, L, q, rmin, rmax, mode, ss, first, seed = CASES[name]
+    rows, n_tail = _rows(frames, C, n, tail, bits, seed)
+    params = oracle.make_params(L, q, rmin, rmax, mode)
+    want = az.encode_frames(rows, params, n, tail, n_tail, sample_bits=bits, channels=C, sample_size=ss,
+                            first_frame=first)
+    monkeypatch.setenv("FLACMI_NO_PACK32", "1")
+    got = az.encode_frames(rows, params, n, tail, n_tail, sample_bits=bits, channels=C, sample_size=ss,
+                           first_frame=first)
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2])
+    assert got[0].tobytes() == want[0].tobytes()
