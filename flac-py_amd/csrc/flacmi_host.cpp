@@ -739,6 +739,7 @@ int flacmi_decode_frames_device(flacmi_ctx* ctx, const uint8_t* stream_data, int
         a.expect = expect->samples;
         a.expect_stride = expect->unit_stride;
         a.expect_bytes = expect->sample_bytes;
+        a.expect_vec = ((uintptr_t)expect->samples & 15) == 0 && ((expect->unit_stride * expect->sample_bytes) & 15) == 0;
         a.block_len = expect->block_len;
         a.tail_len = expect->n_tail_units ? expect->tail_len : expect->block_len;
         a.n_units = expect->n_units;

@@ -94,6 +94,7 @@ struct DecodeArgs {
     const void* expect;      /* optional source rows [n_frames*channels][expect_stride] */
     int64_t expect_stride;
     int32_t expect_bytes;
+    int32_t expect_vec;      /* rows 16-byte aligned: the comparison uses 16-byte loads */
     int32_t block_len, tail_len;
     int64_t n_units, n_tail_units;
     int32_t* out;            /* optional [n_frames*channels][out_stride] */

@@ -175,7 +175,7 @@ __device__ uint32_t crc16_range(const DecodeArgs& a, const uint16_t* t, int64_t 
 
 __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
     __shared__ int32_t ring[kRingSlots][kDecThreads];
-    __shared__ int32_t coef[kRingSlots][kDecThreads];
+    __shared__ int16_t coef[kRingSlots][kDecThreads]; /* precision <= 15 bits (4-bit field, 15 rejected) */
     __shared__ uint16_t crct[4 * 256];
     const int lane = threadIdx.x;
     for (int i = lane; i < 4 * 256; i += kDecThreads) crct[i] = a.crc_slice[i];
@@ -283,9 +283,9 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
                 const int prec = g.uint(4);
                 if (prec == 15) { pfail(DS_LPC_PREC); break; }
                 shift = (int)g.sint(5);
-                for (int k = 0; k < order; ++k) coef[k][lane] = (int32_t)g.sint(prec + 1);
+                for (int k = 0; k < order; ++k) coef[k][lane] = (int16_t)g.sint(prec + 1);
             } else {
-                for (int k = 0; k < order; ++k) coef[k][lane] = fixed_coef(order, k); /* shift 0 */
+                for (int k = 0; k < order; ++k) coef[k][lane] = (int16_t)fixed_coef(order, k); /* shift 0 */
             }
             const int cm = g.uint(2);
             if (cm > 1) { pfail(DS_CODING); break; }
@@ -344,8 +344,33 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
                         for (int k = 0; k < cnt; ++k) orow[c0 + k] = ring[k][lane];
                     }
                 }
-                if (cmp)
-                    for (int k = 0; k < cnt; ++k) bad += ring[k][lane] != expect_at(a, u, c0 + k);
+                if (cmp) {
+                    if (cnt == 32 && a.expect_vec) { /* 16-byte loads of the source row */
+                        if (a.expect_bytes == 2) {
+                            const uint4* e4 = reinterpret_cast<const uint4*>((const int16_t*)a.expect + u * a.expect_stride + c0);
+#pragma unroll
+                            for (int g2 = 0; g2 < 4; ++g2) {
+                                const uint4 v = e4[g2];
+                                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                                for (int h = 0; h < 4; ++h) {
+                                    bad += ring[8 * g2 + 2 * h][lane] != ((int32_t)(w[h] << 16) >> 16);
+                                    bad += ring[8 * g2 + 2 * h + 1][lane] != ((int32_t)w[h] >> 16);
+                                }
+                            }
+                        } else {
+                            const int4v* e4 = reinterpret_cast<const int4v*>((const int32_t*)a.expect + u * a.expect_stride + c0);
+#pragma unroll
+                            for (int g2 = 0; g2 < 8; ++g2) {
+                                const int4v v = e4[g2];
+#pragma unroll
+                                for (int h = 0; h < 4; ++h) bad += ring[4 * g2 + h][lane] != v[h];
+                            }
+                        }
+                    } else {
+                        for (int k = 0; k < cnt; ++k) bad += ring[k][lane] != expect_at(a, u, c0 + k);
+                    }
+                }
             }
             if (g.pos > end_bit) { fail(DS_EOF); break; }
         }
