@@ -156,11 +156,14 @@ __device__ __forceinline__ void put_meta(flacmi_unit_meta* m, int status, int si
 }
 
 /* Workgroup size of k_resid for n samples: 8-sample chunks, up to kCPT per thread while
- * the workgroup stays <= 256 threads (the kernel's launch bound), more beyond that. */
-__host__ __device__ inline int resid_threads(int n) {
+ * the workgroup stays <= 256 threads (512 for the 64-bit paths: their long blocks fill the
+ * LDS with one workgroup per CU, so 8 waves are two per SIMD), more beyond that.  The
+ * kernel's launch bound follows the same rule. */
+__host__ __device__ inline int resid_threads(int n, bool wide = false) {
     const int nch = (n + 7) / 8;
     int nt = 64 * ((nch + 64 * kCPT - 1) / (64 * kCPT));
-    if (nt > 256) nt = 256;
+    const int cap = wide ? 512 : 256;
+    if (nt > cap) nt = cap;
     return nt < 64 ? 64 : nt;
 }
 /* samples one thread of k_resid accumulates */

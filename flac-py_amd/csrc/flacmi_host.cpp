@@ -359,6 +359,20 @@ static bool needs_wide(int n, int bits, int L, int q, int mode) {
     return rmax >= ldexp(1.0, 26) || rmax * resid_samples_per_thread(n) >= ldexp(1.0, 32);
 }
 
+/* PATH_W64S preconditions: samples <= 24 bits and q <= 16 (every sample plane, coefficient
+ * and -2^shift fits int16), and each plane's dot chain stays inside int32:
+ * max|plane| * (L * 2^(q-1) + 2^15) < 2^31.  FLACMI_NO_SPLIT=1 keeps PATH_W64. */
+static bool split_ok(int bits, int L, int q) {
+    static const int off = [] {
+        const char* e = getenv("FLACMI_NO_SPLIT");
+        return (e && atoi(e) != 0) ? 1 : 0;
+    }();
+    if (off || bits > 24 || q > 16 || L < 1) return false;
+    const double plane = bits > 24 - 12 ? ldexp(1.0, bits - 13) : 0.0;
+    const double pmax = plane > 2048.0 ? plane : 2048.0;
+    return pmax * ((double)L * ldexp(1.0, q - 1) + 32768.0) < ldexp(1.0, 31);
+}
+
 /* FLACMI_DEBUG_STOP=k truncates k_resid after phase k (profiling ablation only: the
  * outputs are then incomplete). */
 static int debug_stop() {
@@ -484,7 +498,8 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.retry_count = (unsigned long long*)ctx->retry.p;
         a.retry_list = (int64_t*)ctx->retry.p + 2;
         const bool wide = needs_wide(k.n, b->sample_bits, L, p->qlp_precision, p->mode);
-        const int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
+        int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
+        if (path == 2 && o->residual_bytes == 4 && split_ok(b->sample_bits, L, p->qlp_precision)) path = 3;
         return launch_resid(a, path, o->residual_bytes, st);
     };
     const int slot = ctx->ncalls % flacmi_ctx::kRing;

@@ -126,7 +126,7 @@ static int lmax_bucket(int L) { return L <= 0 ? 0 : L <= 8 ? 8 : L <= 12 ? 12 : 
 
 ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes) {
     ResidLaunch r;
-    r.threads = resid_threads(n);
+    r.threads = resid_threads(n, true); /* worst case: the 64-bit paths' workgroup */
     r.lds_bytes = resid_lds_layout(32, n, r.threads / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff), 4,
                                    residual_bytes == 8 ? 8 : 4, 16 * 1024, false, true).total;
     return r;

@@ -9,6 +9,9 @@
  *             sign-biased operands.  (16-bit samples, q <= 16, |r| < 2^26.)
  *   PATH_N32  int32 samples, v_mad_i32_i24 predictions (samples and q <= 24 bits).
  *   PATH_W64  int32 samples, int64 predictions and sums (anything else).
+ *   PATH_W64S PATH_W64 with the LPC candidate predictions on v_dot2_i32_i16 over two
+ *             12-bit sample planes (samples <= 24 bits, q <= 16, host-checked bound);
+ *             the recombination, shift and |r| sums stay int64.
  * Samples and the zig-zag residual live in separate LDS regions, so the chosen residual
  * is written to LDS and HBM in the same pass. */
 #pragma once
@@ -16,7 +19,7 @@
 
 namespace flacmi {
 
-enum { PATH_S16 = 0, PATH_N32 = 1, PATH_W64 = 2 };
+enum { PATH_S16 = 0, PATH_N32 = 1, PATH_W64 = 2, PATH_W64S = 3 };
 
 typedef short short2v __attribute__((ext_vector_type(2)));
 
@@ -168,11 +171,47 @@ __device__ __forceinline__ void chunk_sums_s16(const Win16<HP>& W, int i0, int n
     });
 }
 
-/* PATH_N32 / PATH_W64: int32 window of HP + 8 samples */
-template <int LMAX, int HP, bool MASKED, bool WIDE>
+/* PATH_W64S: the chunk window split into two int16 planes, x = 4096*h + l with
+ * l = sext12(x) in [-2048, 2048) and h = (x - l) >> 12 (|h| <= 2048 for 24-bit samples),
+ * each as packed pairs laid out like Win16 (E aligned, O shifted by one sample). */
+template <int HP>
+struct SplitWin {
+    static constexpr int NE = (HP + 8) / 2;
+    uint32_t Eh[NE], El[NE], Oh[NE - 1], Ol[NE - 1];
+    __device__ __forceinline__ void build(const int32_t (&w)[HP + 8]) {
+#pragma unroll
+        for (int m = 0; m < NE; ++m) {
+            const int32_t a0 = w[2 * m], a1 = w[2 * m + 1];
+            const int32_t l0 = (a0 << 20) >> 20, l1 = (a1 << 20) >> 20;
+            const int32_t h0 = (a0 - l0) >> 12, h1 = (a1 - l1) >> 12;
+            El[m] = __builtin_amdgcn_perm((uint32_t)l1, (uint32_t)l0, 0x05040100u);
+            Eh[m] = __builtin_amdgcn_perm((uint32_t)h1, (uint32_t)h0, 0x05040100u);
+        }
+#pragma unroll
+        for (int m = 0; m < NE - 1; ++m) {
+            Ol[m] = __builtin_amdgcn_alignbit(El[m + 1], El[m], 16);
+            Oh[m] = __builtin_amdgcn_alignbit(Eh[m + 1], Eh[m], 16);
+        }
+    }
+    /* (x[i-1-2t] lo, x[i-2t] hi) of one plane for the sample at window position HP + k */
+    __device__ __forceinline__ static uint32_t pick(const uint32_t* E, const uint32_t* O, int k, int t) {
+        const int lo = HP + k - 1 - 2 * t;
+        if (lo < 0) return E[0] << 16;
+        return (lo & 1) ? O[(lo - 1) >> 1] : E[lo >> 1];
+    }
+};
+
+/* PATH_N32 / PATH_W64 / PATH_W64S: int32 window of HP + 8 samples.  SPLIT (PATH_W64S):
+ * every LPC candidate is two v_dot2_i32_i16 chains over the S16 coefficient pairs (extra
+ * tap x[i] with -2^sh included), th on the high plane and tl on the low plane.  Both are
+ * exact in int32 under the host bound, and T = 4096*th + tl = pred - 2^sh*x[i] exactly,
+ * so T >> sh = (pred >> sh) - x[i] = -r: per sample and order ceil((p+1)/2) dots per
+ * plane instead of p int64 multiply-adds, then one int64 shift, |.| and add. */
+template <int LMAX, int HP, bool MASKED, bool WIDE, bool SPLIT = false>
 __device__ __forceinline__ void chunk_sums_32(const int32_t (&w)[HP + 8], int i0, int n, int L, bool do_lpc,
                                               const int32_t* cfl, const int32_t* lsh,
-                                              typename std::conditional<WIDE, uint64_t, uint32_t>::type (&acc)[5 + LMAX]) {
+                                              typename std::conditional<WIDE, uint64_t, uint32_t>::type (&acc)[5 + LMAX],
+                                              const uint32_t* cpair = nullptr) {
     using CT = CoefTables<LMAX>;
     int32_t x12[12];
 #pragma unroll
@@ -192,6 +231,66 @@ __device__ __forceinline__ void chunk_sums_32(const int32_t (&w)[HP + 8], int i0
         }
     }
     if (!do_lpc) return;
+    if constexpr (SPLIT) {
+        SplitWin<HP> S;
+        S.build(w);
+        static_for<LMAX>([&](auto P_) {
+            constexpr int pp = P_ + 1;
+            constexpr int np = (pp + 2) / 2;
+            __builtin_amdgcn_sched_barrier(0);
+            if (pp <= L) {
+                uint32_t cq[np];
+                const uint4* src = reinterpret_cast<const uint4*>(cpair + (pp - 1) * CoefTables<LMAX>::PPAD);
+#pragma unroll
+                for (int g = 0; g < (np + 3) / 4; ++g) {
+                    const uint4 v = src[g];
+                    if (4 * g + 0 < np) cq[4 * g + 0] = v.x;
+                    if (4 * g + 1 < np) cq[4 * g + 1] = v.y;
+                    if (4 * g + 2 < np) cq[4 * g + 2] = v.z;
+                    if (4 * g + 3 < np) cq[4 * g + 3] = v.w;
+                }
+                const int sh = lsh[pp - 1];
+                const int start = lsh[LMAX + pp - 1];
+                int32_t th[8], tl[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    th[k] = sdot2(SplitWin<HP>::pick(S.Eh, S.Oh, k, 0), cq[0], 0);
+                    tl[k] = sdot2(SplitWin<HP>::pick(S.El, S.Ol, k, 0), cq[0], 0);
+                }
+#pragma unroll
+                for (int j = 1; j < np; ++j)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        th[k] = sdot2(SplitWin<HP>::pick(S.Eh, S.Oh, k, j), cq[j], th[k]);
+                        tl[k] = sdot2(SplitWin<HP>::pick(S.El, S.Ol, k, j), cq[j], tl[k]);
+                    }
+                if (lsh[2 * LMAX + pp - 1]) {
+                    /* narrow (|r| < 2^28): T >> sh in 32 bits.  sh <= 12: (th << (12-sh)) +
+                     * (tl >> sh), exact mod 2^32 hence exact; sh > 12: (th + (tl >> 12)) >>
+                     * (sh-12), no wrap.  Eight |r| < 2^31 in one u32, then one 64-bit add. */
+                    const int sa = sh < 12 ? 12 - sh : 0, sb = sh < 12 ? sh : 12, sc = sh > 12 ? sh - 12 : 0;
+                    uint32_t s32 = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int i = i0 + k;
+                        const int32_t v = (int32_t)(((uint32_t)th[k] << sa) + (uint32_t)(tl[k] >> sb)) >> sc;
+                        const uint32_t d = sad_acc((uint32_t)v ^ kBias, kBias, 0);
+                        s32 += (!MASKED || (i >= start && i < n)) ? d : 0u;
+                    }
+                    acc[4 + pp] += s32;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int i = i0 + k;
+                        const int64_t t = ((int64_t)th[k] << 12) + (int64_t)tl[k];
+                        const uint64_t v = uabs64(t >> sh);
+                        acc[4 + pp] += (!MASKED || (i >= start && i < n)) ? v : 0;
+                    }
+                }
+            }
+        });
+        return;
+    }
     static_for<LMAX>([&](auto P_) {
         constexpr int pp = P_ + 1;
         __builtin_amdgcn_sched_barrier(0); /* one candidate at a time: bounds register pressure */
@@ -563,7 +662,7 @@ __device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta
  *   kVarList     unit = retry_list[blockIdx.x] for blockIdx.x < *retry_count, every path. */
 enum { kVarGeneric = 0, kVarFast = 1, kVarList = 2 };
 template <int LMAX, int PATH, typename ResT, int VAR>
-__global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
+__global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArgs a) {
     constexpr bool FAST = VAR == kVarFast;
     int64_t gid = blockIdx.x;
     if constexpr (VAR == kVarList) {
@@ -572,7 +671,8 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
     }
     using UX = ResT;
     constexpr bool S16 = PATH == PATH_S16;
-    constexpr bool WIDE = PATH == PATH_W64;
+    constexpr bool WIDE = PATH == PATH_W64 || PATH == PATH_W64S;
+    constexpr bool SPLIT = PATH == PATH_W64S;
     using A = typename std::conditional<WIDE, uint64_t, uint32_t>::type; /* per-thread partial */
     using CT = CoefTables<LMAX>;
     constexpr int HP = resid_hp(LMAX);
@@ -769,6 +869,14 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
             lsh[i] = sh;
             lsh[LMAX + i] = ((negmask >> i) & 1) ? 0 : i + 1; /* first residual index */
             lsh[2 * LMAX + i] = (int32_t)(1u << (31 - sh));
+            if (SPLIT) { /* narrow flag: |r| < 2^28 for 24-bit samples (sum|c| < 30 * 2^sh) */
+                int64_t sa = 0;
+                if (i < L) {
+                    const int32_t* cp = rec + 2 + L + (i * (i + 1)) / 2;
+                    for (int j = 0; j <= i; ++j) sa += cp[j] < 0 ? -cp[j] : cp[j];
+                }
+                lsh[2 * LMAX + i] = (i < L && sa < 30LL * (1LL << sh)) ? 1 : 0;
+            }
             if (MF && i < L) {
                 const int32_t* cp = rec + 2 + L + (i * (i + 1)) / 2;
                 int sa = 1 << sh;
@@ -852,8 +960,8 @@ __global__ __launch_bounds__(256) void k_resid(ResidArgs a) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) w[4 * g + e] = v[e];
             }
-            if (fast) chunk_sums_32<LMAX, HP, false, WIDE>(w, i0, n, L, do_lpc, cfl, lsh, acc);
-            else chunk_sums_32<LMAX, HP, true, WIDE>(w, i0, n, L, do_lpc, cfl, lsh, acc);
+            if (fast) chunk_sums_32<LMAX, HP, false, WIDE, SPLIT>(w, i0, n, L, do_lpc, cfl, lsh, acc, cpair);
+            else chunk_sums_32<LMAX, HP, true, WIDE, SPLIT>(w, i0, n, L, do_lpc, cfl, lsh, acc, cpair);
         }
     }
 
@@ -1314,8 +1422,8 @@ static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
-    const int nt = resid_threads(a.n);
-    const bool regz = resid_regz(a.n, rmax_eff, PATH != PATH_W64 && sizeof(ResT) == 4);
+    const int nt = resid_threads(a.n, PATH >= PATH_W64);
+    const bool regz = resid_regz(a.n, rmax_eff, PATH != PATH_W64 && PATH != PATH_W64S && sizeof(ResT) == 4);
     const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff),
                                         PATH == PATH_S16 ? 2 : 4, (int)sizeof(ResT), CoefTables<LMAX>::BYTES,
                                         regz, false).total;
@@ -1369,6 +1477,8 @@ static hipError_t launch_resid_bucket(const ResidArgs& a, int path, int rb, hipS
         if (path == PATH_S16 && resid_fast_ok(a)) return launch_resid_fast<LMAX>(a, s);
     if (path == PATH_S16) return launch_resid_T<LMAX, PATH_S16, uint32_t>(a, s);
     if (path == PATH_N32) return launch_resid_T<LMAX, PATH_N32, uint32_t>(a, s);
+    if constexpr (LMAX > 0)
+        if (path == PATH_W64S) return launch_resid_T<LMAX, PATH_W64S, uint32_t>(a, s);
     return launch_resid_T<LMAX, PATH_W64, uint32_t>(a, s);
 }
 
