@@ -361,11 +361,13 @@ static bool needs_wide(int n, int bits, int L, int q, int mode) {
 
 /* PATH_W64S preconditions: samples <= 24 bits and q <= 16 (every sample plane, coefficient
  * and -2^shift fits int16), and each plane's dot chain stays inside int32:
- * max|plane| * (L * 2^(q-1) + 2^15) < 2^31.  FLACMI_NO_SPLIT=1 keeps PATH_W64. */
+ * max|plane| * (L * 2^(q-1) + 2^15) < 2^31.  Opt-in (FLACMI_SPLIT=1): on MI355X it
+ * measured slower than PATH_W64's v_mad_i64_i32 chains (c3: 71.0 vs 67.1 ms), the plane
+ * build costing more than the dot2 pairing saves. */
 static bool split_ok(int bits, int L, int q) {
     static const int off = [] {
-        const char* e = getenv("FLACMI_NO_SPLIT");
-        return (e && atoi(e) != 0) ? 1 : 0;
+        const char* e = getenv("FLACMI_SPLIT");
+        return (e && atoi(e) != 0) ? 0 : 1;
     }();
     if (off || bits > 24 || q > 16 || L < 1) return false;
     const double plane = bits > 24 - 12 ? ldexp(1.0, bits - 13) : 0.0;
@@ -497,6 +499,7 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.mfma = use_mfma();
         a.retry_count = (unsigned long long*)ctx->retry.p;
         a.retry_list = (int64_t*)ctx->retry.p + 2;
+        a.sample_bits = b->sample_bits;
         const bool wide = needs_wide(k.n, b->sample_bits, L, p->qlp_precision, p->mode);
         int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
         if (path == 2 && o->residual_bytes == 4 && split_ok(b->sample_bits, L, p->qlp_precision)) path = 3;

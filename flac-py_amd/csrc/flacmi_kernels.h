@@ -50,6 +50,7 @@ struct ResidArgs {
     int32_t mfma;            /* 1 = MFMA candidate sums where exact (env FLACMI_NO_MFMA=1 -> 0) */
     unsigned long long* retry_count; /* fast-path units handed to the generic kernel: count, */
     int64_t* retry_list;             /* and their batch indices (NULL: no fast path) */
+    int32_t sample_bits;             /* declared sample width (bounds the 64-bit paths' narrow sums) */
 };
 /* internal unit status between the fast and the generic k_resid (never returned) */
 #define FLACMI_STATUS_RETRY 0x7e

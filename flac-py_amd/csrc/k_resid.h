@@ -317,6 +317,8 @@ __device__ __forceinline__ void chunk_sums_32(const int32_t (&w)[HP + 8], int i0
                     if (MASKED) s = (i >= start && i < n) ? s : 0;
                     acc[4 + pp] += s;
                 } else {
+                    /* (a 32-bit |r| epilogue under the narrow flag measured slower here:
+                     * the duplicated chains spill at the 512-thread register budget) */
                     int64_t pred = 0;
 #pragma unroll
                     for (int j = 0; j < pp; ++j) pred += (int64_t)c[j] * (int64_t)w[HP + k - 1 - j];
@@ -869,13 +871,14 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             lsh[i] = sh;
             lsh[LMAX + i] = ((negmask >> i) & 1) ? 0 : i + 1; /* first residual index */
             lsh[2 * LMAX + i] = (int32_t)(1u << (31 - sh));
-            if (SPLIT) { /* narrow flag: |r| < 2^28 for 24-bit samples (sum|c| < 30 * 2^sh) */
+            if (SPLIT) { /* narrow flag: samples <= 24 bits and sum|c| < 30 * 2^sh, so
+                          * |pred >> sh| < 2^28 + 2^23 and |r| < 2^28 */
                 int64_t sa = 0;
                 if (i < L) {
                     const int32_t* cp = rec + 2 + L + (i * (i + 1)) / 2;
                     for (int j = 0; j <= i; ++j) sa += cp[j] < 0 ? -cp[j] : cp[j];
                 }
-                lsh[2 * LMAX + i] = (i < L && sa < 30LL * (1LL << sh)) ? 1 : 0;
+                lsh[2 * LMAX + i] = (i < L && a.sample_bits <= 24 && sa < 30LL * (1LL << sh)) ? 1 : 0;
             }
             if (MF && i < L) {
                 const int32_t* cp = rec + 2 + L + (i * (i + 1)) / 2;

@@ -201,3 +201,68 @@ def test_synth_device_matches_oracle(az):
         az.lib.flacmi_device_free(az.ctx, d)
         want = oracle.synth_batch(5, n_units, n, bits, 42, dtype=dt)
         assert np.array_equal(host, want)
+
+
+# ---------------------------------------------------------------------------------------
+# 24-bit wide paths: the narrow (32-bit |r|) sums and the int64 ones
+# ---------------------------------------------------------------------------------------
+def _tones24(n_units, n, seed, noise):
+    """Near-full-scale 24-bit tone sums; without noise, high-order LPC candidates get
+    sum|c| >= 30 * 2^shift (outside the narrow bound), with it they stay inside."""
+    r = np.random.default_rng(seed)
+    t = np.arange(n)
+    a = np.zeros((n_units, n), np.int32)
+    for u in range(n_units):
+        x = np.zeros(n)
+        for _ in range(r.integers(1, 4)):
+            x += r.uniform(0.1, 0.3) * np.sin(2 * np.pi * r.uniform(5, 2000) / 96000 * t + r.uniform(0, 6.28))
+        x = x * (2 ** 23 - 1) + r.normal(0, noise, n)
+        a[u] = np.clip(np.round(x), -2 ** 23, 2 ** 23 - 1)
+    return a
+
+
+def _outside_narrow(ora, L):
+    cnt = 0
+    for rec in ora["lpc_records"]:
+        if rec[0] != 0:
+            continue
+        for p in range(1, L + 1):
+            sh = int(rec[2 + p - 1])
+            c = rec[2 + L + p * (p - 1) // 2: 2 + L + p * (p - 1) // 2 + p].astype(np.int64)
+            cnt += int(np.abs(c).sum() >= 30 * 2 ** sh)
+    return cnt
+
+
+@pytest.mark.parametrize("q", [15, 12])
+@pytest.mark.parametrize("noise", [0.0, 0.5, 4.0])
+def test_24bit_tones_narrow_and_wide_candidate_sums(az, q, noise):
+    n, L = 4096, 32
+    a = _tones24(16, n, 11, noise)
+    out = az.analyze(a, make_params(L, q, 0, 8), n, sample_bits=24, debug=True)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, 8), n, sample_bits=24, threads=16)
+    if noise == 0.0:
+        assert _outside_narrow(ora, L) > 0  # the int64 sums are exercised
+    compare_with_oracle(out, ora, [n] * 16)
+
+
+def test_split_plane_path_opt_in():
+    """PATH_W64S (opt-in, FLACMI_SPLIT=1, read once per process): config 3 shape and
+    full-scale tones, in a child process, bit-exact against the oracle."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path[:0] = ['tests', 'oracle', '.']\n"
+            "import test_gpu_parity as T\n"
+            "from flac_amd.analysis import Analyzer, make_params\n"
+            "az = Analyzer(0)\n"
+            "T.batch_case(az, 12, 16384, 24, 97, 32, 15, 0, 8)\n"
+            "a = T._tones24(16, 4096, 12, 0.0)\n"
+            "out = az.analyze(a, make_params(32, 15, 0, 8), 4096, sample_bits=24, debug=True)\n"
+            "ora = T.oracle.analyze_batch(a, T.oracle.make_params(32, 15, 0, 8), 4096, sample_bits=24, threads=16)\n"
+            "T.compare_with_oracle(out, ora, [4096] * 16)\n"
+            "az.close()\n"
+            "print('split ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=repo, env={**os.environ, "FLACMI_SPLIT": "1"},
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "split ok" in r.stdout, r.stdout[-1000:] + r.stderr[-3000:]
