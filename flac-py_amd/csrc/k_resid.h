@@ -1371,6 +1371,47 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     uint64_t tb[16];
 #pragma unroll
     for (int o = 0; o < 16; ++o) tb[o] = 0;
+    if (sizeof(ResT) == 4 && (ps & 7) == 0) {
+        /* whole 8-sample chunks per partition: the heap sums are dead, so each finest
+         * partition's parameters are packed there, one byte per order (16 B x P = the hs
+         * region); a chunk reads its residual with two 16-byte loads and its parameters
+         * with one.  Chunks whose values are all < 2^29 sum eight shifts in 32 bits. */
+        uint4* pkv = reinterpret_cast<uint4*>(hs);
+        __syncthreads(); /* the error scan above read hs */
+        for (int k = tid; k < P; k += NT) {
+            uint32_t pw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int o = 0; o < 16; ++o)
+                if (o >= rmin && o <= omax) pw[o >> 2] |= ((uint32_t)hp[(1 << o) + (k >> (omax - o))] & 0xffu) << (8 * (o & 3));
+            pkv[k] = uint4{pw[0], pw[1], pw[2], pw[3]};
+        }
+        __syncthreads();
+        const int cpp = ps >> 3;
+        const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+        for (int c = tid; c < nch; c += NT) {
+            const uint4 u = reinterpret_cast<const uint4*>(zz)[2 * c], v = reinterpret_cast<const uint4*>(zz)[2 * c + 1];
+            const uint32_t z[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+            const uint4 pv = pkv[c / cpp];
+            if (((u.x | u.y | u.z | u.w | v.x | v.y | v.z | v.w) >> 29) == 0) {
+                uint32_t t32[16];
+#pragma unroll
+                for (int o = 0; o < 16; ++o) t32[o] = 0;
+                chunk_rice_bits(z, pv, ro, oo, t32);
+#pragma unroll
+                for (int o = 0; o < 16; ++o)
+                    if (o >= ro && o <= oo) tb[o] += t32[o];
+            } else {
+                const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+                for (int o = 0; o < 16; ++o)
+                    if (o >= ro && o <= oo) {
+                        const uint32_t p = (pw[o >> 2] >> (8 * (o & 3))) & 0xffu;
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) tb[o] += (uint64_t)(z[k] >> p);
+                    }
+            }
+        }
+    } else
     for (int k = wid; k < P; k += nw) {
         int pk[16];
 #pragma unroll

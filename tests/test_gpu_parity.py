@@ -266,3 +266,21 @@ def test_split_plane_path_opt_in():
     r = subprocess.run([sys.executable, "-c", code], cwd=repo, env={**os.environ, "FLACMI_SPLIT": "1"},
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "split ok" in r.stdout, r.stdout[-1000:] + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("mode", [abi.MODE_FIXED_ONLY, abi.MODE_REFERENCE])
+def test_large_residuals_chunked_rice_bits(az, mode):
+    """32-bit samples near +-2^30 in long blocks (LDS-resident residual, 256 finest
+    partitions): zig-zag values >= 2^29 take the chunked data-bits pass's 64-bit branch,
+    quiet units its 32-bit one."""
+    n, nu = 16384, 8
+    r = np.random.default_rng(5)
+    a = np.zeros((nu, n), np.int32)
+    for u in range(nu):
+        amp = [2 ** 30, 2 ** 12][u % 2]
+        a[u] = r.integers(-amp, amp, n, dtype=np.int64).astype(np.int32)
+    L = 0 if mode == abi.MODE_FIXED_ONLY else 8
+    out = az.analyze(a, make_params(L, 12, 0, 8, mode), n, sample_bits=32, debug=True)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, 12, 0, 8, mode), n, sample_bits=32, threads=16)
+    assert int((ora["meta"]["status"] == 0).sum()) >= nu // 2
+    compare_with_oracle(out, ora, [n] * nu)
