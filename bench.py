@@ -6,14 +6,20 @@ choice, Rice partition search; residuals written back zig-zagged for the host pa
 over one resident batch of --units synthetic 4608-sample int16 blocks per GPU, plus the
 per-step stream statistics that are all-reduced over RCCL when N > 1.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--units U] [--config c2|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--units U] [--config c2|c3|c4|c5]
 
-For N > 1 the driver starts one process per GPU with torch.distributed.run; each rank
-analyses its own shard (weak scaling: --units per GPU).  Rank 0 prints one JSON line.
+For N > 1 one process runs per GPU.  Either the driver starts them with
+torch.distributed.run (WORLD_SIZE set), or `bench.py --gpus N` starts them itself: it
+spawns torch.distributed.run with N ranks as a child process before any GPU call and
+exits with its status.  Every rank checks that the process group holds exactly N ranks;
+each analyses its own shard (weak scaling: --units per GPU; c4: round-robin chunks of one
+fixed job, strong scaling).  Rank 0 prints one JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,7 +47,7 @@ METRIC = "PCM samples/sec encode-analysis, 4608-blk/16-bit mono, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -54,7 +60,39 @@ def parse():
     ap.add_argument("--parity-units", type=int, default=64)
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-frames", action="store_true", help="skip the frame-writer measurement")
-    return ap.parse_args()
+    ap.add_argument("--launch-check", action="store_true",
+                    help="multi-rank plumbing only (CPU, gloo): self-launch, world-size check, shard "
+                         "coverage and the stats all-reduce; prints a launch_check JSON line, no metric")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args, argv):
+    """`--gpus N > 1` outside a torch.distributed job: run N ranks of this script under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as a CHILD process
+    and return its exit status.  Called before anything touches the GPU (this process never
+    initialises HIP), so nothing is exec'ed over a GPU-initialised process.  Returns None
+    when no launch is needed (N == 1, or already a rank of a launched job)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL on this host: dmabuf IPC only
+    return subprocess.call(cmd, env=env)
+
+
+def check_world(args, world):
+    """The process group must hold exactly the ranks --gpus asked for."""
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s); run "
+                         f"`python bench.py --gpus {args.gpus}` (self-launch) or torch.distributed.run with "
+                         f"--nproc-per-node {args.gpus}")
 
 
 def algorithmic_bytes(cfg, meta_np, n_units):
@@ -224,10 +262,58 @@ def reduce_elapsed(elapsed, dist=None, device=None):
     return elapsed
 
 
-def main():
-    args = parse()
+def shard_plan(cfg, rank, world, units, total_units_arg=0):
+    """(first_unit, chunks) of one rank.  Non-chunked configs: the contiguous shard
+    [rank*U, (rank+1)*U) (weak scaling).  c4: chunk ci of the fixed job goes to rank
+    ci % world (round-robin, BASELINE config 4), chunks of `units` blocks."""
+    if "total_units" not in cfg:
+        return shard_first_unit(rank, units), [], world * units
+    total = total_units_arg or cfg["total_units"]
+    n_chunks = (total + units - 1) // units
+    return 0, list(range(rank, n_chunks, world)), total
+
+
+def launch_check(args, cfg, units):
+    """Multi-rank plumbing without a GPU (gloo): each rank reports its shard as a stats
+    vector [units, samples, first, last+1, rank bit]; the all-reduced vector must cover
+    the job exactly once.  Rank 0 prints one launch_check JSON line."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    check_world(args, world)
+    first, chunks, total = shard_plan(cfg, rank, world, units, args.total_units)
+    if chunks:
+        mine = sum(min(units, total - ci * units) for ci in chunks)
+        lo, hi = chunks[0] * units, min(total, chunks[-1] * units + units)
+    else:
+        mine, lo, hi = units, first, first + units
+    st = torch.tensor([mine, mine * cfg["n"], lo, hi, 1 << rank], dtype=torch.int64)
+    reduce_stats(st, dist)
+    el = reduce_elapsed(0.001 * (rank + 1), dist)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world_size": world, "gpus_arg": args.gpus, "config": args.config,
+                          "units_total": int(st[0]), "samples_total": int(st[1]), "expected_units": total,
+                          "rank_mask": int(st[4]), "elapsed_max": el}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rc = self_launch(args, argv)
+    if rc is not None:
+        return rc
     cfg = dict(CONFIGS[args.config])
     units = args.units or cfg["units"]
+    if args.launch_check:
+        launch_check(args, cfg, units)
+        return 0
 
     import numpy as np
     import torch
@@ -240,6 +326,8 @@ def main():
     if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+    check_world(args, world)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -255,7 +343,8 @@ def main():
     sstride = ((n * sbytes + 15) // 16) * 16 // sbytes
     rstride = ((n * 4 + 15) // 16) * 16 // 4
     pstride = params_stride_for(cfg["rmax"])
-    first_unit = shard_first_unit(rank, units)
+    first_unit, my_chunks, total_units = shard_plan(cfg, rank, world, units, args.total_units)
+    chunked = "total_units" in cfg
 
     samples = torch.empty((units, sstride), dtype=sdt, device=dev)
     meta = torch.empty((units, abi.META_DTYPE.itemsize), dtype=torch.uint8, device=dev)
@@ -265,10 +354,6 @@ def main():
     az.synth_device(samples.data_ptr(), sbytes, bits, sstride, first_unit, units, n, args.seed, sptr)
     params = make_params(cfg["L"], cfg["q"], cfg["rmin"], cfg["rmax"], cfg["mode"])
 
-    chunked = "total_units" in cfg
-    total_units = (args.total_units or cfg["total_units"]) if chunked else world * units
-    n_chunks = (total_units + units - 1) // units
-    my_chunks = list(range(rank, n_chunks, world)) if chunked else []
     stats_acc = torch.zeros_like(stats)
 
     def step():
@@ -395,4 +480,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

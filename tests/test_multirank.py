@@ -82,3 +82,54 @@ def test_shards_disjoint_and_covering():
         spans = [(bench.shard_first_unit(r, 1000), bench.shard_first_unit(r, 1000) + 1000) for r in range(world)]
         assert spans[0][0] == 0 and spans[-1][1] == world * 1000
         assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+
+
+def _bench(args, env_extra=None, timeout=300):
+    import subprocess
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env)
+
+
+def _json_line(out):
+    import json
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert lines, out
+    return json.loads(lines[-1])
+
+
+@pytest.mark.parametrize("gpus,config", [(2, "c2"), (4, "c4")])
+def test_bench_self_launches_n_ranks(gpus, config):
+    """`bench.py --gpus N` (no torch.distributed environment) starts N ranks itself; every
+    rank sees world size N; the all-reduced shard vector covers the job exactly once."""
+    extra = ["--total-units", "1000003", "--units", "100000"] if config == "c4" else []
+    r = _bench(["--gpus", str(gpus), "--config", config, "--launch-check"] + extra)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_line(r.stdout)
+    assert d["world_size"] == gpus and d["gpus_arg"] == gpus
+    assert d["rank_mask"] == (1 << gpus) - 1
+    assert d["units_total"] == d["expected_units"]
+    assert d["elapsed_max"] == pytest.approx(0.001 * gpus)
+
+
+def test_bench_rejects_world_size_mismatch():
+    """A rank whose process group does not hold --gpus ranks stops with an error."""
+    r = _bench(["--gpus", "2", "--launch-check"], {"WORLD_SIZE": "1", "RANK": "0"})
+    assert r.returncode != 0
+    assert "process group has 1 rank" in r.stderr
+
+
+def test_shard_plan_round_robin_chunks():
+    sys.path.insert(0, REPO)
+    import bench
+    cfg = bench.CONFIGS["c4"]
+    for world in (1, 2, 4, 8):
+        seen = []
+        for r in range(world):
+            first, chunks, total = bench.shard_plan(cfg, r, world, 1000, 10_500)
+            assert total == 10_500 and all(c % world == r for c in chunks)
+            seen += chunks
+        assert sorted(seen) == list(range(11))
