@@ -1,7 +1,7 @@
 """Command line with flac/__main__.py's `encode` action (its arguments, defaults and
-output bytes), on the device path: PCM ingest (ingest.read_wav, the reference reader's
-byte grouping unless --correct-reader), device analysis and device frame writer
-(encoder.encode_planar).
+output bytes), on the device path: streamed PCM ingest (ingest.iter_wav_batches, the
+reference reader's byte grouping unless --correct-reader), device analysis and device
+frame writer (encoder.encode_wav).
 
     python -m flac_amd encode infile.wav outfile.flac [-b N] [-l N] [-q N] [-r [M,]N]
                                                        [--correct-reader] [--fixed-only]
@@ -41,16 +41,14 @@ def make_argument_parser():
 
 
 def cmd_encode(args) -> None:
-    from .encoder import EncoderParameters, encode_planar
-    from .ingest import read_wav
-    info, pcm = read_wav(args.infile, quirk=not args.correct_reader)
+    from .encoder import EncoderParameters, encode_wav
     parameters = EncoderParameters(block_size=args.block_size, lpc_order=range(args.max_lpc_order + 1),
                                    qlp_precision=args.qlp_coeff_precision,
                                    rice_partition_order=args.rice_partition_order)
     t0 = timer()
     with args.outfile.open("wb") as f:
-        for bs in encode_planar(info.sample_rate, info.sample_width * 8, pcm, parameters, frames=info.frames,
-                                device=args.device, fixed_only=args.fixed_only):
+        for bs in encode_wav(args.infile, parameters, quirk=not args.correct_reader, device=args.device,
+                             fixed_only=args.fixed_only):
             f.write(bs)
     print(f"Encoding completed in {timer() - t0:.6g} seconds")
 

@@ -394,6 +394,15 @@ static int use_mfma() {
     return v;
 }
 
+/* FLACMI_NO_STREAM=1 keeps k_resid's one-workgroup-per-unit kernels (comparison runs). */
+static int use_stream() {
+    static const int v = [] {
+        const char* e = getenv("FLACMI_NO_STREAM");
+        return (e && atoi(e) != 0) ? 0 : 1;
+    }();
+    return v;
+}
+
 /* FLACMI_OVERLAP=k (k > 1): k_lpc and k_resid of consecutive chunks overlap on two
  * streams (see analyze_device_impl); chunks hold at least kOverlapMinUnits units. */
 constexpr int64_t kOverlapMinUnits = 16384;
@@ -500,6 +509,7 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.retry_count = (unsigned long long*)ctx->retry.p;
         a.retry_list = (int64_t*)ctx->retry.p + 2;
         a.sample_bits = b->sample_bits;
+        a.stream = use_stream();
         const bool wide = needs_wide(k.n, b->sample_bits, L, p->qlp_precision, p->mode);
         int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
         if (path == 2 && o->residual_bytes == 4 && split_ok(b->sample_bits, L, p->qlp_precision)) path = 3;

@@ -51,6 +51,7 @@ struct ResidArgs {
     unsigned long long* retry_count; /* fast-path units handed to the generic kernel: count, */
     int64_t* retry_list;             /* and their batch indices (NULL: no fast path) */
     int32_t sample_bits;             /* declared sample width (bounds the 64-bit paths' narrow sums) */
+    int32_t stream;                  /* 1 = k_resid_stream where the shape allows (env FLACMI_NO_STREAM=1 -> 0) */
 };
 /* internal unit status between the fast and the generic k_resid (never returned) */
 #define FLACMI_STATUS_RETRY 0x7e

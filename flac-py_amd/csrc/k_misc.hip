@@ -9,6 +9,8 @@ hipError_t launch_resid_l8(const ResidArgs&, int, int, hipStream_t);
 hipError_t launch_resid_l12(const ResidArgs&, int, int, hipStream_t);
 hipError_t launch_resid_l16(const ResidArgs&, int, int, hipStream_t);
 hipError_t launch_resid_l32(const ResidArgs&, int, int, hipStream_t);
+bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes);
+hipError_t launch_resid_stream(const ResidArgs& a, hipStream_t s);
 
 /* ====================================================================================
  * small kernels: record expansion (debug), synthetic PCM, stream statistics
@@ -134,6 +136,7 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes) {
 
 hipError_t launch_resid(const ResidArgs& a, int path, int residual_bytes, hipStream_t s) {
     if (a.count <= 0) return hipSuccess;
+    if (stream_shape_ok(a, path, residual_bytes)) return launch_resid_stream(a, s);
     const int lb = (a.mode == FLACMI_MODE_FIXED_ONLY || a.mode == FLACMI_MODE_RICE_ONLY) ? 0 : lmax_bucket(a.L);
     switch (lb) {
         case 0: return launch_resid_l0(a, path, residual_bytes, s);

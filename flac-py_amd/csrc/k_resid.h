@@ -664,13 +664,8 @@ __device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta
  *   kVarList     unit = retry_list[blockIdx.x] for blockIdx.x < *retry_count, every path. */
 enum { kVarGeneric = 0, kVarFast = 1, kVarList = 2 };
 template <int LMAX, int PATH, typename ResT, int VAR>
-__global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArgs a) {
+__device__ __forceinline__ void k_resid_body(const ResidArgs& a, const int64_t gid) {
     constexpr bool FAST = VAR == kVarFast;
-    int64_t gid = blockIdx.x;
-    if constexpr (VAR == kVarList) {
-        if (gid >= (int64_t)*a.retry_count) return;
-        gid = a.retry_list[gid];
-    }
     using UX = ResT;
     constexpr bool S16 = PATH == PATH_S16;
     constexpr bool WIDE = PATH == PATH_W64 || PATH == PATH_W64S;
@@ -1461,6 +1456,25 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     } /* !FAST */
 }
 
+/* kVarGeneric / kVarFast: unit = blockIdx.x.  kVarList: a bounded grid loops over the listed
+ * units (the list's length is only known on the device); the barrier in front of each unit
+ * keeps a unit's LDS staging behind every wave of the previous one. */
+template <int LMAX, int PATH, typename ResT, int VAR>
+__global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArgs a) {
+    if constexpr (VAR == kVarList) {
+        const int64_t cnt = (int64_t)*a.retry_count;
+        for (int64_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+            __syncthreads();
+            k_resid_body<LMAX, PATH, ResT, VAR>(a, a.retry_list[i]);
+        }
+    } else {
+        k_resid_body<LMAX, PATH, ResT, VAR>(a, (int64_t)blockIdx.x);
+    }
+}
+
+/* grid of the list variant: enough workgroups to fill the chip when many units are listed */
+constexpr int64_t kListGrid = 2048;
+
 template <int LMAX, int PATH, typename ResT>
 static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     int rmax_eff = -1;
@@ -1499,7 +1513,23 @@ static hipError_t launch_resid_fast(const ResidArgs& a, hipStream_t s) {
     auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
     e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gen);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kl, dim3((unsigned)a.count), dim3(nt), lds_gen, s, a);
+    hipLaunchKernelGGL(kl, dim3((unsigned)(a.count < kListGrid ? a.count : kListGrid)), dim3(nt), lds_gen, s, a);
+    return hipGetLastError();
+}
+
+/* the generic S16 body over the units k_resid_stream listed (k_stream.hip) */
+template <int LMAX>
+static hipError_t launch_resid_list(const ResidArgs& a, hipStream_t s) {
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (a.n % (1 << o) == 0) rmax_eff = o;
+    const int nt = resid_threads(a.n);
+    const int P = 1 << (rmax_eff < 0 ? 0 : rmax_eff);
+    const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, P, 2, 4, CoefTables<LMAX>::BYTES, true, false).total;
+    auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
+    hipError_t e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kl, dim3((unsigned)(a.count < kListGrid ? a.count : kListGrid)), dim3(nt), lds, s, a);
     return hipGetLastError();
 }
 

@@ -1,0 +1,714 @@
+/* k_stream.hip — the residual-side analysis (candidate sums, choice, chosen residual, Rice
+ * search) for the common 16-bit shapes as a PERSISTENT, software-pipelined kernel.
+ *
+ * Same results as k_resid (k_resid.h) bit for bit; it replaces k_resid's one-workgroup-per-
+ * unit launch where the shape allows (host check: stream_shape_ok):
+ *   int16 samples, q <= 16, 32-bit residual rows, reference mode with 1 <= L <= 12 or
+ *   fixed-only mode, n % 64 == 0, 64 <= n <= 6144, finest Rice partitions of whole
+ *   8-sample chunks, at most 64 of them.
+ *
+ * Reference semantics (flac/encoder.py): fixed predictors 331-359, LPC candidate residuals
+ * 386-404 with prediction_residual 537-548, the fixed-vs-LPC choice 133-157, encode_residual
+ * + rice_partitions + find_rice_parameter + rice_size 632-760.
+ *
+ * Structure (one workgroup of nw = n/1536 rounded-up waves, looping over units
+ * u = blockIdx.x, += gridDim.x; grid = resident workgroups):
+ *   - the NEXT unit's samples and LPC record are loaded into registers right after the
+ *     current unit is staged, so HBM latency hides behind a whole unit of compute;
+ *   - samples sit in LDS biased (x ^ 0x8000: unsigned 16-bit), which makes the MFMA operand
+ *     build two byte permutes and two packed subtracts per lane and block;
+ *   - candidate sums on v_mfma_f32_16x16x32_f16 with INTEGER taps and the accumulator
+ *     initialised to M = 1.5 * 2^23: every partial sum is an integer inside [2^23, 2^24)
+ *     (ulp 1) under the per-unit bound (sum|c| + 2^shift) * 33023 < 2^22, so the result is
+ *     exactly M + T with T = pred - 2^shift * x[i] whatever the accumulation order.  The
+ *     float's bit pattern is then 0x4B400000 + T; 0x4B400000 is a multiple of 2^22, so
+ *     (bits >> shift) - (0x4B400000 >> shift) = floor(T / 2^shift) = -r exactly.  Fixed
+ *     predictors (shift 0): |r| is one v_sad_u32; LPC: one shift + one v_sad_u32.
+ *     MFMA 0 holds fixed orders 1..4 x 4 sample phases, MFMAs 1..NG the LPC orders
+ *     4(g-1)+1 .. 4g x 4 phases.  Units outside the bound are listed for k_resid.
+ *   - the choice, the Rice parameters (per-wave butterfly over the finest partitions) and
+ *     the order choice are computed redundantly by every wave from LDS data, so a unit
+ *     needs four workgroup barriers and no single-wave serial section;
+ *   - Rice data bits on packed 16-bit pairs (v_pk_lshrrev_b16 + v_dot2_u32_u16) when a
+ *     chunk's values are < 2^16;
+ *   - the 208-byte meta record is one coalesced store of 52 lanes.
+ */
+#include "device_common.h"
+
+namespace flacmi {
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+constexpr int kSHP = 16;                     /* biased-zero history pad in front of the unit (samples) */
+constexpr uint32_t kMagicBits = 0x4B400000u; /* 1.5 * 2^23 */
+constexpr int kCoefLimit = 127;              /* (sum|c| + 2^shift) * 33023 < 2^22 */
+constexpr int kRiceOrders = 8;               /* orders 0..7 kept per finest partition */
+
+struct SLds {
+    int xs, rec, red, red0, red2, cs, pk, mst, misc, total;
+};
+
+__host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P) {
+    auto up = [](int b) { return (b + 15) & ~15; };
+    SLds l;
+    int o = 0;
+    l.xs = o;   o = up(o + 2 * (kSHP + n));
+    l.rec = o;  o = up(o + 4 * (rec_words > 0 ? rec_words : 1));
+    l.red = o;  o = up(o + 4 * nw * 64);            /* u32 [nw][group][order][kb] */
+    l.red0 = o; o = up(o + 4 * nw);                 /* u32 [nw] sum|x| */
+    l.red2 = o; o = up(o + 8 * (nw + 1) * kRiceOrders); /* u64 [nw][order] data bits, [order] headers */
+    l.cs = o;   o = up(o + 4 * (n / 8));            /* u32 chunk sums of the chosen residual */
+    l.pk = o;   o = up(o + nw * P * 4 * kRiceOrders); /* u32 [nw][P][order] = p | p << 16 */
+    l.mst = o;  o = up(o + 4 * 20);                  /* wave 0: meta scalar fields */
+    l.misc = o; o = up(o + 4 * 4);                   /* Rice error key / site, Rice5Bit order mask */
+    l.total = o;
+    return l;
+}
+
+/* |a - b| + acc: the compiler emits one v_sad_u32 when b is in a VGPR (opaque() keeps a
+ * constant b there).  Not inline asm: the hazard recognizer does not see an asm operand
+ * read an MFMA result, and such a read without the required wait states returns garbage. */
+__device__ __forceinline__ uint32_t sad32(uint32_t a, uint32_t b, uint32_t acc) { return (a > b ? a - b : b - a) + acc; }
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t h2sub(uint32_t t, float c) {
+    const h2 v = __builtin_bit_cast(h2, t) - h2{(_Float16)c, (_Float16)c};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+/* A fragment of one lane from 4 biased samples (two dwords): f16 high bytes (signed, via
+ * (1024 + hb) - 1152) then f16 low bytes ((1024 + l) - 1024), all exact. */
+__device__ __forceinline__ h8 a_frag(uint2 q) {
+    const uint32_t hx = __builtin_amdgcn_perm(0x64646464u, q.x, 0x04030401u);
+    const uint32_t hy = __builtin_amdgcn_perm(0x64646464u, q.y, 0x04030401u);
+    const uint32_t lx = __builtin_amdgcn_perm(0x64646464u, q.x, 0x04020400u);
+    const uint32_t ly = __builtin_amdgcn_perm(0x64646464u, q.y, 0x04020400u);
+    const uint4 v{h2sub(hx, 1152.0f), h2sub(hy, 1152.0f), h2sub(lx, 1024.0f), h2sub(ly, 1024.0f)};
+    return __builtin_bit_cast(h8, v);
+}
+
+/* exact floor(log2(s / len)) = max{p : len * 2^p <= s} for s >= 1 (s < 2^46; see
+ * k_resid.h rice_params_wave0 for why this equals the reference's float computation) */
+__device__ __forceinline__ int rice_param_exact(uint64_t s, int len) {
+    const int fs = 63 - __builtin_clzll((unsigned long long)s);
+    const int fl = 31 - __builtin_clz((unsigned)len);
+    int p = fs - fl;
+    if (p >= 0 && ((uint64_t)len << p) > s) --p;
+    return p;
+}
+
+/* fixed order K residual of samples i0..i0+7 from biased LDS samples, zig-zagged; the
+ * warm-up samples (i < K) give 0 */
+template <int K>
+__device__ __forceinline__ void fixed_chunk(const uint16_t* xs, int i0, uint32_t (&z)[8]) {
+    const uint4 w = *reinterpret_cast<const uint4*>(xs + i0);
+    const uint4 v = *reinterpret_cast<const uint4*>(xs + i0 - 8); /* pad >= 8 */
+    const uint32_t q[6] = {v.z, v.w, w.x, w.y, w.z, w.w};
+    int32_t d[12]; /* biased samples i0-4 .. i0+7 */
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        d[2 * t] = (int32_t)(q[t] & 0xffffu);
+        d[2 * t + 1] = (int32_t)(q[t] >> 16);
+    }
+    if constexpr (K == 0) {
+#pragma unroll
+        for (int t = 4; t < 12; ++t) d[t] -= 32768;
+    }
+#pragma unroll
+    for (int l = 1; l <= K; ++l)
+#pragma unroll
+        for (int t = 11; t >= 4 - K + l; --t) d[t] -= d[t - 1];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t r = d[4 + k];
+        z[k] = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+    }
+    if (i0 == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) z[k] = 0;
+    }
+}
+
+/* LPC order p (<= 12) residual of samples i0..i0+7 (prediction_residual, encoder.py:537-548):
+ * r = x[i] - (sum_j c[j] x[i-1-j] >> shift); |pred| < 2^22 under the MFMA bound.  Samples
+ * i < start give 0.  Rare (LPC rarely wins under the reference's sign convention), so it
+ * is written for registers, not speed: the 24 samples stay packed, the coefficients are
+ * wave-uniform (lane q of coefl holds c[q]; c[q] == 0 for q >= p). */
+__device__ __forceinline__ void lpc_chunk(const uint16_t* xs, int i0, int32_t coefl, int sh, int start,
+                                          uint32_t (&z)[8]) {
+    uint32_t w[12]; /* biased samples i0-16 .. i0+7, two per word */
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        const uint4 v = *reinterpret_cast<const uint4*>(xs + i0 - 16 + 8 * g);
+        w[4 * g] = v.x;
+        w[4 * g + 1] = v.y;
+        w[4 * g + 2] = v.z;
+        w[4 * g + 3] = v.w;
+    }
+    auto x = [&](int t) __attribute__((always_inline)) -> int32_t {
+        return (int32_t)((t & 1) ? (w[t >> 1] >> 16) : (w[t >> 1] & 0xffffu)) - 32768;
+    };
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        int32_t pred = 0;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) pred += __builtin_amdgcn_readlane(coefl, j) * x(16 + k - 1 - j);
+        const int32_t r = x(16 + k) - (pred >> sh);
+        const uint32_t zz = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+        z[k] = (i0 + k >= start) ? zz : 0u;
+    }
+}
+
+/* One wave writes the 52 dwords of a unit's flacmi_unit_meta (include/flacmi.h field order)
+ * with one store: lane 0 stages the 20 scalar fields in LDS (mst), lanes 20..51 take
+ * coefs[lane - 20] from lane q's `coef`. */
+struct MetaVals {
+    int status, site, kind, order, shift, ncoefs, res_offset, res_len, fixed_order, lpc_order, part_order,
+        n_parts, coding;
+    long long fixed_sum, lpc_sum, rice_bits;
+};
+__device__ __forceinline__ void store_meta(flacmi_unit_meta* m, int lane, const MetaVals& v, int32_t coef,
+                                           uint32_t* mst) {
+    if (lane == 0) {
+        uint4* d = reinterpret_cast<uint4*>(mst);
+        d[0] = uint4{(uint32_t)v.status, (uint32_t)v.site, (uint32_t)v.kind, (uint32_t)v.order};
+        d[1] = uint4{(uint32_t)v.shift, (uint32_t)v.ncoefs, (uint32_t)v.res_offset, (uint32_t)v.res_len};
+        d[2] = uint4{(uint32_t)v.fixed_order, (uint32_t)v.lpc_order, (uint32_t)v.part_order, (uint32_t)v.n_parts};
+        d[3] = uint4{(uint32_t)v.coding, 0u, (uint32_t)v.fixed_sum, (uint32_t)((unsigned long long)v.fixed_sum >> 32)};
+        d[4] = uint4{(uint32_t)v.lpc_sum, (uint32_t)((unsigned long long)v.lpc_sum >> 32), (uint32_t)v.rice_bits,
+                     (uint32_t)((unsigned long long)v.rice_bits >> 32)};
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t cq = (uint32_t)__shfl(coef, (lane - 20) & 63);
+    const uint32_t x = lane < 20 ? mst[lane < 20 ? lane : 0] : cq;
+    if (lane < 52) reinterpret_cast<uint32_t*>(m)[lane] = x;
+}
+
+}  // namespace
+
+/* NG = number of LPC MFMA groups (ceil(L / 4)), 0 in fixed-only mode.  One workgroup per
+ * unit; every exit is workgroup-uniform (all waves decide from the same LDS data). */
+template <int NG>
+__global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, nw = NT >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t gid = blockIdx.x;
+    const int n = a.n, L = NG > 0 ? a.L : 0;
+    const int nch = n >> 3, nblk = n >> 6;
+    const int rw = NG > 0 ? a.rec_words : 0;
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (n % (1 << o) == 0) rmax_eff = o;
+    const int Pmax = 1 << rmax_eff; /* host-checked: 0 <= rmax_eff <= 5 */
+    const SLds lay = stream_lds(n, nw, rw, Pmax);
+    uint16_t* xs = reinterpret_cast<uint16_t*>(smem + lay.xs) + kSHP;
+    int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.rec);
+    uint32_t* red = reinterpret_cast<uint32_t*>(smem + lay.red);
+    uint32_t* red0 = reinterpret_cast<uint32_t*>(smem + lay.red0);
+    unsigned long long* red2 = reinterpret_cast<unsigned long long*>(smem + lay.red2);
+    uint32_t* pks = reinterpret_cast<uint32_t*>(smem + lay.cs);  /* finest partition sums */
+    uint32_t* pkw = reinterpret_cast<uint32_t*>(smem + lay.pk) + wid * Pmax * kRiceOrders;
+    uint32_t* mst = reinterpret_cast<uint32_t*>(smem + lay.mst);
+    flacmi_unit_meta* meta = a.meta + gid;
+    MetaVals mv{};
+
+    /* ---- stage: biased samples and the record into LDS, sum|x| on the way ---- */
+    {
+        const uint4* src = reinterpret_cast<const uint4*>((const int16_t*)a.samples + (a.unit0 + gid) * a.stride);
+        uint4 q[kCPT];
+#pragma unroll
+        for (int j = 0; j < kCPT; ++j)
+            if (tid + j * NT < nch) q[j] = src[tid + j * NT];
+        int32_t rv[2] = {0, 0};
+        if constexpr (NG > 0) {
+            const int32_t* r = a.rec + gid * a.rec_words;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (tid + j * NT < rw) rv[j] = r[tid + j * NT];
+        }
+        if (tid < kSHP) xs[tid - kSHP] = 0x8000u; /* biased zeros */
+        if (tid < Pmax) pks[tid] = 0;
+        const uint32_t k8000 = opaque(0x8000u);
+        uint32_t sumx = 0;
+#pragma unroll
+        for (int j = 0; j < kCPT; ++j) {
+            const int v = tid + j * NT;
+            if (v < nch) {
+                const uint4 y{q[j].x ^ 0x80008000u, q[j].y ^ 0x80008000u, q[j].z ^ 0x80008000u, q[j].w ^ 0x80008000u};
+                *reinterpret_cast<uint4*>(xs + 8 * v) = y;
+                const uint32_t yd[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    sumx = sad32(yd[e] & 0xffffu, k8000, sumx);
+                    sumx = sad32(yd[e] >> 16, k8000, sumx);
+                }
+            }
+        }
+        if constexpr (NG > 0) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (tid + j * NT < rw) recl[tid + j * NT] = rv[j];
+        }
+        const uint32_t sx = wave_sum_u32(sumx);
+        if (lane == 0) red0[wid] = sx;
+    }
+    __syncthreads(); /* B1 */
+
+    /* ---- unit status from the LPC record; MFMA exactness bound per order ---- */
+    uint32_t negmask = 0;
+    if constexpr (NG > 0) {
+        const int st = recl[0];
+        if (st != 0) { /* the reference raises inside encode_subframe_lpc */
+            if (wid == 0) {
+                mv.status = st & 0xffff;
+                mv.site = st >> 16;
+                store_meta(meta, lane, mv, 0, mst);
+            }
+            return;
+        }
+        negmask = (uint32_t)recl[1];
+        int sa = 0;
+        if (lane < L) {
+            const int p = lane + 1;
+            const int32_t* cp = recl + 2 + L + (p * (p - 1)) / 2;
+            int c[4 * NG];
+#pragma unroll
+            for (int j = 0; j < 4 * NG; ++j) c[j] = j < p ? cp[j] : 0; /* independent reads */
+            sa = 1 << recl[2 + lane];
+#pragma unroll
+            for (int j = 0; j < 4 * NG; ++j) sa += c[j] < 0 ? -c[j] : c[j];
+        }
+        if (__ballot(sa > kCoefLimit)) { /* outside the exactness bound: k_resid redoes it */
+            if (tid == 0) {
+                meta->status = FLACMI_STATUS_RETRY;
+                const unsigned long long k = atomicAdd(a.retry_count, 1ull);
+                a.retry_list[k] = gid;
+            }
+            return;
+        }
+    }
+    if (a.stop_after == 1) return;
+
+    /* ---- candidate sums on MFMA ---- */
+    {
+        const int col = lane & 15, kb = lane >> 4, o4 = col >> 2, rho = col & 3;
+        h8 B[NG + 1];
+        int shg[NG + 1], startg[NG + 1];
+        uint32_t kg[NG + 1];
+#pragma unroll
+        for (int g = 0; g <= NG; ++g) {
+            int p = 0, sh = 0, start = 0;
+            const int32_t* cp = recl;
+            if (g == 0) {
+                p = o4 + 1; /* fixed order */
+                start = p;
+            } else {
+                p = 4 * (g - 1) + o4 + 1; /* LPC order */
+                if (p <= L) {
+                    sh = recl[2 + p - 1];
+                    cp = recl + 2 + L + (p * (p - 1)) / 2;
+                    start = ((negmask >> (p - 1)) & 1) ? 0 : p;
+                } else {
+                    p = 0;
+                }
+            }
+            float t[4];
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const int d = 4 * kb + jj - 12 - rho; /* tap offset: x[i + d] */
+                const int m = -d - 1;
+                float v = 0.0f;
+                if (g == 0) {
+                    /* fixed order k (common.py:15-21): x[i-1-m] weighs (-1)^m C(k, m+1) */
+                    const int k = p;
+                    if (d == 0) {
+                        v = -1.0f;
+                    } else if (m >= 0 && m < k) {
+                        const int c1 = k, c2 = k * (k - 1) / 2, c3 = k * (k - 1) * (k - 2) / 6,
+                                  c4 = k * (k - 1) * (k - 2) * (k - 3) / 24;
+                        v = (float)(m == 0 ? c1 : m == 1 ? -c2 : m == 2 ? c3 : -c4);
+                    }
+                } else if (p > 0) {
+                    if (d == 0) v = -(float)(1 << sh);
+                    else if (m >= 0 && m < p) v = (float)cp[m];
+                }
+                t[jj] = v;
+            }
+            uint32_t w[4];
+            w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[0], 256.0f * t[1]));
+            w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[2], 256.0f * t[3]));
+            w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t[0], t[1]));
+            w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t[2], t[3]));
+            B[g] = __builtin_bit_cast(h8, uint4{w[0], w[1], w[2], w[3]});
+            shg[g] = sh;
+            kg[g] = kMagicBits >> sh;
+            startg[g] = start;
+        }
+        const uint32_t mbv = opaque(kMagicBits);
+        const f4 C{12582912.0f, 12582912.0f, 12582912.0f, 12582912.0f};
+        const int eoff = 4 * (lane & 15) - 12 + 4 * kb;
+        uint32_t acc[NG + 1];
+#pragma unroll
+        for (int g = 0; g <= NG; ++g) acc[g] = 0;
+        auto block = [&](uint2 q, bool masked) __attribute__((always_inline)) {
+            const h8 A = a_frag(q);
+            f4 D[NG + 1];
+#pragma unroll
+            for (int g = 0; g <= NG; ++g) D[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[g], C, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g <= NG; ++g)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    /* (a bit_cast of a vector element reads element 0: clang bug) */
+                    const uint32_t bits = __float_as_uint(D[g][r]);
+                    if (masked) {
+                        const int i = 4 * (4 * kb + r) + rho; /* block 0 */
+                        const uint32_t sv = g == 0 ? sad32(bits, mbv, 0u) : sad32(bits >> shg[g], kg[g], 0u);
+                        acc[g] += i >= startg[g] ? sv : 0u;
+                    } else if (g == 0) { /* opaque: one v_sad_u32 per value, not a reassociated min/max/sub */
+                        acc[0] = opaque(sad32(bits, mbv, acc[0]));
+                    } else {
+                        acc[g] = sad32(bits >> shg[g], kg[g], acc[g]);
+                    }
+                }
+        };
+        /* this wave's blocks wid, wid + nw, ... (wave 0 takes block 0 masked, last); two
+         * blocks per step with both operand reads issued first */
+        int blk = wid == 0 ? nw : wid;
+#if FLACMI_STREAM_UNROLL2
+        for (; blk + nw < nblk; blk += 2 * nw) {
+            const uint2 q0 = *reinterpret_cast<const uint2*>(xs + 64 * blk + eoff);
+            const uint2 q1 = *reinterpret_cast<const uint2*>(xs + 64 * (blk + nw) + eoff);
+            block(q0, false);
+            block(q1, false);
+        }
+#endif
+        for (; blk < nblk; blk += nw) block(*reinterpret_cast<const uint2*>(xs + 64 * blk + eoff), false);
+        if (wid == 0) block(*reinterpret_cast<const uint2*>(xs + eoff), true);
+        /* per (group, order, kb): sum over the 4 phases (quad), lanes with rho == 0 store */
+#pragma unroll
+        for (int g = 0; g <= NG; ++g) {
+            uint32_t v = acc[g];
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
+            if (rho == 0) red[(wid * 4 + g) * 16 + o4 * 4 + kb] = v;
+        }
+    }
+    __syncthreads(); /* B2 */
+    if (a.stop_after == 2) return;
+
+    /* ---- choice (encoder.py:331-359, 398-404, 135-157), every wave ----
+     * lane j < 4: fixed order j+1; 4 <= j < 16: LPC order j-3; lane 16: fixed order 0 */
+    uint64_t tj = 0;
+    if (lane < 4 * (NG + 1)) {
+#pragma unroll 1
+        for (int w2 = 0; w2 < nw; ++w2) {
+            const uint4 r4 = *reinterpret_cast<const uint4*>(red + (w2 * 4 + (lane >> 2)) * 16 + (lane & 3) * 4);
+            tj += (uint64_t)r4.x + r4.y + r4.z + r4.w;
+        }
+    } else if (lane == 16) {
+#pragma unroll 1
+        for (int w2 = 0; w2 < nw; ++w2) tj += red0[w2];
+    }
+    const uint32_t tlo = (uint32_t)tj, thi = (uint32_t)(tj >> 32);
+    auto tot_at = [&](int j) __attribute__((always_inline)) -> uint64_t {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thi, j) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)tlo, j);
+    };
+    int fo = 0;
+    uint64_t fsum = tot_at(16);
+#pragma unroll
+    for (int o = 1; o < 5; ++o) {
+        const uint64_t v = tot_at(o - 1);
+        if (v < fsum) {
+            fsum = v;
+            fo = o;
+        }
+    }
+    int lbest = 0;
+    uint64_t lsum = 0;
+    bool lpc_wins = false, tie = false;
+    if constexpr (NG > 0) {
+        lbest = 1;
+        lsum = tot_at(4);
+#pragma unroll
+        for (int pp = 2; pp <= 4 * NG; ++pp) {
+            if (pp <= L) {
+                const uint64_t v = tot_at(3 + pp);
+                if (v < lsum) {
+                    lsum = v;
+                    lbest = pp;
+                }
+            }
+        }
+        /* a coefficient-less candidate sums |x| over all n (= the fixed order-0 sum), so it
+         * never wins strictly */
+        lpc_wins = lsum < fsum;
+        tie = !lpc_wins && !(fsum < lsum);
+    }
+    if (wid == 0) {
+        const uint64_t fv = (uint64_t)__shfl((unsigned long long)tj, lane == 0 ? 16 : (lane - 1) & 63);
+        if (a.fixed_sums && lane < 5) a.fixed_sums[gid * 5 + lane] = (long long)fv;
+        if (a.lpc_sums && lane < 32) {
+            const uint64_t v = (uint64_t)__shfl((unsigned long long)tj, (lane + 4) & 63);
+            a.lpc_sums[gid * 32 + lane] = (lane + 1 <= L) ? (long long)v : 0;
+        }
+    }
+    mv.fixed_order = fo;
+    mv.lpc_order = lbest;
+    mv.fixed_sum = (long long)fsum;
+    mv.lpc_sum = (long long)lsum;
+    if (tie) {
+        if (wid == 0) {
+            mv.status = ST_ASSERT;
+            mv.site = FLACMI_SITE_CHOICE_TIE;
+            store_meta(meta, lane, mv, 0, mst);
+        }
+        return;
+    }
+    int32_t coefl = 0; /* lane q: coefficient q of the chosen LPC order */
+    mv.kind = lpc_wins ? FLACMI_KIND_LPC : FLACMI_KIND_FIXED;
+    mv.order = lpc_wins ? lbest : fo;
+    if constexpr (NG > 0) {
+        if (lpc_wins) {
+            mv.shift = recl[2 + lbest - 1];
+            mv.ncoefs = lbest;
+            if (lane < lbest) coefl = recl[2 + L + (lbest * (lbest - 1)) / 2 + lane];
+        }
+    }
+    if (a.stop_after == 3) return;
+
+    /* ---- chosen residual: zig-zag (utils.py:91-94) to HBM; kept in registers as 16-bit
+     * pairs when every value of the chunk is < 2^16 (else recomputed for the Rice pass);
+     * finest partition sums by LDS atomics ---- */
+    const int order = mv.order;
+    int omax = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if ((n % (1 << o)) == 0 && (n >> o) > order) omax = o;
+    const int P = 1 << (omax < 0 ? 0 : omax), cpp = (n >> (omax < 0 ? 0 : omax)) >> 3;
+    const float inv_cpp = 1.0f / (float)cpp;
+    uint32_t* __restrict__ rout = reinterpret_cast<uint32_t*>(a.residual) + gid * a.residual_stride;
+    const int fixed_k = __builtin_amdgcn_readfirstlane(lpc_wins ? -1 : order);
+    const int lsh = mv.shift;
+    auto resid = [&](int c, uint32_t (&z)[8]) __attribute__((always_inline)) {
+        switch (fixed_k) {
+            case 0: fixed_chunk<0>(xs, 8 * c, z); break;
+            case 1: fixed_chunk<1>(xs, 8 * c, z); break;
+            case 2: fixed_chunk<2>(xs, 8 * c, z); break;
+            case 3: fixed_chunk<3>(xs, 8 * c, z); break;
+            case 4: fixed_chunk<4>(xs, 8 * c, z); break;
+            default:
+                if constexpr (NG > 0) lpc_chunk(xs, 8 * c, coefl, lsh, order, z);
+                break;
+        }
+    };
+    uint32_t zp[kCPT][4]; /* 16-bit pairs of the chunk's residual */
+    uint32_t big = 0;     /* bit j: chunk j holds a value >= 2^16 */
+#pragma unroll
+    for (int j = 0; j < kCPT; ++j) {
+        const int c = tid + j * NT;
+        zp[j][0] = zp[j][1] = zp[j][2] = zp[j][3] = 0;
+        if (c < nch) {
+            uint32_t z[8];
+            resid(c, z);
+            reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{z[0], z[1], z[2], z[3]};
+            reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{z[4], z[5], z[6], z[7]};
+            const uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
+            if (omax >= 0) atomicAdd(&pks[(int)(((float)c + 0.5f) * inv_cpp)], cs);
+            if ((z[0] | z[1] | z[2] | z[3] | z[4] | z[5] | z[6] | z[7]) >> 16) big |= 1u << j;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) zp[j][i] = __builtin_amdgcn_perm(z[2 * i + 1], z[2 * i], 0x05040100u);
+        }
+    }
+    __syncthreads(); /* B3 */
+    if (a.stop_after == 4) return;
+
+    /* ---- Rice partition search (encoder.py:655-760) ---- */
+    if (omax < 0) {
+        if (wid == 0) {
+            mv.status = ST_ASSERT;
+            mv.site = FLACMI_SITE_RICE_NO_ORDER;
+            store_meta(meta, lane, mv, coefl, mst);
+        }
+        return;
+    }
+    const int ro = __builtin_amdgcn_readfirstlane(a.rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+    /* every wave, lane j - 1 = heap node j = (order o, partition K), j = 2^o + K < 2P <= 64:
+     * node sums from a prefix over the finest sums, one parameter each, the first error in
+     * the reference's evaluation order = the lowest node (orders ascending, then partitions) */
+    uint64_t pre = lane < P ? (uint64_t)pks[lane] : 0;
+#pragma unroll
+    for (int d = 1; d < 32; d <<= 1) {
+        const uint64_t t = (uint64_t)__shfl_up((unsigned long long)pre, (unsigned)d);
+        if (lane >= d) pre += t;
+    }
+    const int j = lane + 1;
+    const int o = 31 - __builtin_clz((unsigned)j);
+    const int K = j - (1 << o), dd = oo - o;
+    const bool valid = j < 2 * P && o >= ro;
+    const int hi_k = ((K + 1) << (dd < 0 ? 0 : dd)) - 1, lo_k = (K << (dd < 0 ? 0 : dd)) - 1;
+    const uint64_t ph = (uint64_t)__shfl((unsigned long long)pre, hi_k & 63);
+    const uint64_t pl = (uint64_t)__shfl((unsigned long long)pre, lo_k & 63);
+    const uint64_t snode = ph - (lo_k >= 0 ? pl : 0ull);
+    const int len = (n >> (o < 16 ? o : 15)) - (K == 0 ? order : 0);
+    const bool zero = snode == 0;
+    const int prm = (zero || !valid) ? 0 : rice_param_exact(snode, len);
+    {
+        const unsigned long long eb = __ballot(valid && (zero || prm < 0));
+        if (eb) {
+            if (wid == 0) {
+                const int kl = __builtin_ctzll(eb);
+                mv.status = ST_VALUE;
+                mv.site = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
+                store_meta(meta, lane, mv, coefl, mst);
+            }
+            return;
+        }
+    }
+    /* this wave's table: finest partition k (lane k) -> the parameter of its ancestor at
+     * every order, as p | p << 16 */
+#pragma unroll
+    for (int o2 = 0; o2 < kRiceOrders; ++o2) {
+        if (o2 >= ro && o2 <= oo) {
+            const int node = (1 << o2) + (lane >> (oo - o2));
+            const int pv = __shfl(prm, (node - 1) & 63);
+            if (lane < P) pkw[lane * kRiceOrders + o2] = (uint32_t)pv * 0x10001u;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    /* data bits: sum of x >> p over the residual for every candidate order */
+    uint32_t tb[kRiceOrders];
+#pragma unroll
+    for (int o2 = 0; o2 < kRiceOrders; ++o2) tb[o2] = 0;
+#pragma unroll
+    for (int jc = 0; jc < kCPT; ++jc) {
+        const int c = tid + jc * NT;
+        if (c < nch) {
+            const int k = (int)(((float)c + 0.5f) * inv_cpp);
+            const uint4 p0 = *reinterpret_cast<const uint4*>(pkw + k * kRiceOrders);
+            const uint4 p1 = *reinterpret_cast<const uint4*>(pkw + k * kRiceOrders + 4);
+            const uint32_t pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+            if (!((big >> jc) & 1)) {
+#pragma unroll
+                for (int o2 = 0; o2 < kRiceOrders; ++o2)
+                    if (o2 >= ro && o2 <= oo) {
+                        const us2 sv = __builtin_bit_cast(us2, pv[o2]);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            tb[o2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, zp[jc][i]) >> sv, us2{1, 1}, tb[o2],
+                                                            false);
+                    }
+            } else {
+                uint32_t z[8];
+                resid(c, z);
+#pragma unroll
+                for (int o2 = 0; o2 < kRiceOrders; ++o2)
+                    if (o2 >= ro && o2 <= oo) {
+                        const uint32_t sh = pv[o2] & 0xffffu;
+                        tb[o2] += (z[0] >> sh) + (z[1] >> sh) + (z[2] >> sh) + (z[3] >> sh) + (z[4] >> sh) +
+                                  (z[5] >> sh) + (z[6] >> sh) + (z[7] >> sh);
+                    }
+            }
+        }
+    }
+    {
+        uint32_t any = 0;
+#pragma unroll
+        for (int o2 = 0; o2 < kRiceOrders; ++o2) any |= (o2 >= ro && o2 <= oo) ? tb[o2] : 0u;
+        const bool narrow = __ballot(any >= (1u << 26)) == 0;
+#pragma unroll
+        for (int o2 = 0; o2 < kRiceOrders; ++o2)
+            if (o2 >= ro && o2 <= oo) {
+                const uint64_t w = narrow ? (uint64_t)wave_sum_u32(tb[o2]) : wave_sum_u64(tb[o2]);
+                if (lane == 0) red2[wid * kRiceOrders + o2] = w;
+            }
+    }
+    __syncthreads(); /* B4 */
+    if (wid != 0) return;
+    /* wave 0: headers per order (lanes of that order's nodes), totals, first minimum */
+    const uint32_t hb = valid ? 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm) : 0u;
+    const unsigned long long m14 = __ballot(valid && prm > 14);
+    unsigned long long bb = 0;
+    int best = -1;
+    uint32_t m5 = 0;
+#pragma unroll
+    for (int o2 = 0; o2 < kRiceOrders; ++o2)
+        if (o2 >= ro && o2 <= oo) {
+            const uint32_t ht = wave_sum_u32(o == o2 ? hb : 0u);
+            unsigned long long v = ht;
+#pragma unroll 1
+            for (int w2 = 0; w2 < nw; ++w2) v += red2[w2 * kRiceOrders + o2];
+            if (best < 0 || v < bb) {
+                bb = v;
+                best = o2;
+            }
+            const unsigned long long om = ((1ull << (1 << o2)) - 1) << ((1 << o2) - 1); /* lanes of order o2 */
+            if (m14 & om) m5 |= 1u << o2;
+        }
+    mv.status = ST_OK;
+    mv.res_offset = order;
+    mv.res_len = n - order;
+    mv.part_order = best;
+    mv.n_parts = 1 << best;
+    mv.coding = ((m5 >> best) & 1) ? 5 : 4;
+    mv.rice_bits = (long long)bb;
+    store_meta(meta, lane, mv, coefl, mst);
+    int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
+    if (lane < (1 << best)) rp[lane] = (int32_t)(pkw[(lane << (oo - best)) * kRiceOrders + best] & 0xffffu);
+}
+
+/* units the stream kernel listed (outside its MFMA bound) are handled by k_resid's list
+ * variant, see launch_resid_bucket_list in k_resid.h */
+hipError_t launch_resid_retry_l8(const ResidArgs& a, hipStream_t s);
+hipError_t launch_resid_retry_l12(const ResidArgs& a, hipStream_t s);
+
+bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes) {
+    if (!a.stream || path != 0 || residual_bytes != 4 || a.sample_bytes != 2 || !a.mfma || !a.retry_list || !a.retry_count)
+        return false;
+    const bool ref = a.mode == FLACMI_MODE_REFERENCE && a.L >= 1 && a.L <= 12;
+    if (!ref && a.mode != FLACMI_MODE_FIXED_ONLY) return false;
+    if (a.n % 64 != 0 || a.n < 64 || a.n > 8 * kCPT * 256) return false;
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (a.n % (1 << o) == 0) rmax_eff = o;
+    if (rmax_eff < 0 || (1 << rmax_eff) > 32 || ((a.n >> rmax_eff) & 7) != 0) return false; /* heap nodes < 64 */
+    const int nt = resid_threads(a.n);
+    if (ref && a.rec_words > 2 * nt) return false;
+    return true;
+}
+
+template <int NG>
+static hipError_t launch_stream_T(const ResidArgs& a, hipStream_t s) {
+    const int nt = resid_threads(a.n);
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (a.n % (1 << o) == 0) rmax_eff = o;
+    const size_t lds = stream_lds(a.n, nt / 64, NG > 0 ? a.rec_words : 0, 1 << rmax_eff).total;
+    auto kern = k_resid_stream<NG>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)a.count), dim3(nt), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_resid_stream(const ResidArgs& a, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(a.retry_count, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    if (a.mode == FLACMI_MODE_FIXED_ONLY) return launch_stream_T<0>(a, s); /* nothing is ever listed */
+    if (a.L <= 4) e = launch_stream_T<1>(a, s);
+    else if (a.L <= 8) e = launch_stream_T<2>(a, s);
+    else e = launch_stream_T<3>(a, s);
+    if (e != hipSuccess) return e;
+    return a.L <= 8 ? launch_resid_retry_l8(a, s) : launch_resid_retry_l12(a, s);
+}
+
+}  // namespace flacmi

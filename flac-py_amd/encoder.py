@@ -29,7 +29,7 @@ from .common import (
 from .crc import crc8
 from .utils import batch
 
-__all__ = ["EncoderParameters", "encode", "encode_planar", "encode_subframe_fixed", "encode_subframe_lpc",
+__all__ = ["EncoderParameters", "encode", "encode_planar", "encode_wav", "encode_subframe_fixed", "encode_subframe_lpc",
            "encode_residual", "put_frame_header", "put_metadata_block_header",
            "put_metadata_block_streaminfo"]
 
@@ -230,6 +230,33 @@ def encode_planar(sample_rate: int, sample_size: int, pcm: np.ndarray, parameter
                                                  channels=channels, sample_size=sample_size, first_frame=b0)
         buf = data.tobytes()
         for b in range(rows.shape[0] // channels):
+            st = int(status[b])
+            _raise_status(st & 0xFFFF, st >> 16)
+            yield buf[int(offsets[b]):int(offsets[b + 1])]
+
+
+def encode_wav(path, parameters: EncoderParameters, *, quirk: bool = True, device: int = 0,
+               blocks_per_batch: int = 8192, fixed_only: bool = False) -> Iterator[bytes]:
+    """The reference CLI's encode action (flac/__main__.py:58-109) on a WAV file, streamed:
+    the stream header first, then frames batch by batch (ingest.iter_wav_batches), so the
+    host holds one batch of PCM at a time.  A reader failure (the reference's IndexError on
+    its byte grouping, encoder.py:102) is raised after the stream header, as the reference
+    CLI has written it by then."""
+    from .ingest import iter_wav_batches, wav_info
+    info = wav_info(path)
+    if info.sample_rate <= 48_000:
+        assert parameters.lpc_order.stop <= 13
+    yield from _stream_header(info.sample_rate, info.sample_width * 8, info.channels, info.frames, parameters)
+    rmin, rmax = _rice_range(parameters.rice_partition_order)
+    mode = abi.MODE_FIXED_ONLY if fixed_only else abi.MODE_REFERENCE
+    params = make_params(parameters.lpc_order.stop - 1, parameters.qlp_precision, rmin, rmax, mode)
+    n, C = parameters.block_size, info.channels
+    for b0, rows, bits, tail_len, n_tail in iter_wav_batches(path, n, blocks_per_batch, quirk):
+        az = _analyzer(device)  # after the first batch is read: a reader failure needs no device
+        data, offsets, status = az.encode_frames(rows, params, n, tail_len, n_tail, sample_bits=bits,
+                                                 channels=C, sample_size=info.sample_width * 8, first_frame=b0)
+        buf = data.tobytes()
+        for b in range(rows.shape[0] // C):
             st = int(status[b])
             _raise_status(st & 0xFFFF, st >> 16)
             yield buf[int(offsets[b]):int(offsets[b + 1])]

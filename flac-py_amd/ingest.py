@@ -7,13 +7,13 @@ then `group(xs, channels)` (utils.py:61-66) splits the frame's bytes into chunks
 `sampwidth` bytes.  For 16-bit stereo the two coincide; for mono 16-bit every sample
 becomes the int8 of its low byte; with sampwidth < channels the reference raises
 IndexError.  `quirk=True` (the default, as the reference CLI does) reproduces exactly
-that; `quirk=False` reads each channel's sampwidth-byte little-endian signed sample.
+that; `quirk=False` reads each channel's sampwidth-byte little-endian signed sample (8-bit
+WAV samples are unsigned with a 128 offset).
 
 Blocks are then cut as utils.batch (utils.py:31-40) does — `block_size` frames each, the
 last one short — and laid out as the C-ABI's planar units: row b*channels + c holds
-channel c of block b (flacmi_batch in include/flacmi.h).  Files are read in bounded
-chunks of frames through the stdlib wave reader, so memory stays proportional to the
-output rows.
+channel c of block b (flacmi_batch in include/flacmi.h).  iter_wav_batches reads a file
+batch by batch through the stdlib wave reader, so memory stays bounded by one batch.
 """
 import wave
 from dataclasses import dataclass
@@ -52,11 +52,36 @@ def frames_to_channels(raw: bytes, channels: int, width: int, quirk: bool = True
         if n_chunks < channels:
             raise IndexError("list index out of range")  # encoder.py:102 x[c]
         return np.stack([_le_signed(a[:, c * chunk:min((c + 1) * chunk, fb)]) for c in range(channels)])
+    if width == 1:  # WAV 8-bit PCM is unsigned with a 128 offset
+        return np.stack([a[:, c].astype(np.int64) - 128 for c in range(channels)])
     return np.stack([_le_signed(a[:, c * width:(c + 1) * width]) for c in range(channels)])
 
 
+def wav_info(path) -> PcmInfo:
+    with wave.open(str(path), "rb") as w:
+        return PcmInfo(w.getframerate(), w.getsampwidth(), w.getnchannels(), w.getnframes())
+
+
+def iter_wav_batches(path, block_size: int, blocks_per_batch: int, quirk: bool = True):
+    """Stream a WAV file as device-ready batches: yields (first_block, rows, bits, tail_len,
+    n_tail_units) exactly as planar_blocks() cuts them, reading blocks_per_batch *
+    block_size frames at a time, so memory is bounded by one batch whatever the file size."""
+    with wave.open(str(path), "rb") as w:
+        channels, width = w.getnchannels(), w.getsampwidth()
+        first = 0
+        while True:
+            raw = w.readframes(blocks_per_batch * block_size)
+            if not raw:
+                return
+            pcm = frames_to_channels(raw, channels, width, quirk)
+            rows, bits, tail_len, n_tail = planar_blocks(pcm, block_size)
+            yield first, rows, bits, tail_len, n_tail
+            first += rows.shape[0] // channels
+
+
 def read_wav(path, quirk: bool = True, chunk_frames: int = 1 << 20):
-    """-> (PcmInfo, int64 [channels][frames])."""
+    """-> (PcmInfo, int64 [channels][frames]): the whole file in memory (tests and small
+    files; the CLI streams through iter_wav_batches)."""
     with wave.open(str(path), "rb") as w:
         info = PcmInfo(w.getframerate(), w.getsampwidth(), w.getnchannels(), w.getnframes())
         parts = []

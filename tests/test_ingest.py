@@ -64,9 +64,49 @@ def test_correct_reader(channels, width):
     raw = rng.integers(0, 256, size=n * channels * width, dtype=np.uint8).tobytes()
     got = ingest.frames_to_channels(raw, channels, width, quirk=False)
     fb = channels * width
-    want = [[int.from_bytes(raw[f * fb + c * width:f * fb + (c + 1) * width], "little", signed=True)
-             for f in range(n)] for c in range(channels)]
+    if width == 1:  # 8-bit WAV samples are unsigned, offset 128
+        want = [[raw[f * fb + c] - 128 for f in range(n)] for c in range(channels)]
+    else:
+        want = [[int.from_bytes(raw[f * fb + c * width:f * fb + (c + 1) * width], "little", signed=True)
+                 for f in range(n)] for c in range(channels)]
     assert got.tolist() == want
+
+
+@pytest.mark.parametrize("frames,block,channels,width,per", [(100000, 4608, 1, 2, 3), (30001, 1000, 2, 3, 4),
+                                                              (4608 * 4, 4608, 2, 2, 2), (5, 4608, 1, 2, 8)])
+@pytest.mark.parametrize("quirk", [True, False])
+def test_streamed_batches_equal_whole_file(tmp_path, frames, block, channels, width, per, quirk):
+    """iter_wav_batches (the CLI's bounded-memory reader) cuts the same rows as
+    planar_blocks over the whole file."""
+    if quirk and width < channels:
+        pytest.skip("the reference reader raises for this shape")
+    rng = np.random.default_rng(frames + width)
+    raw = rng.integers(0, 256, size=frames * channels * width, dtype=np.uint8).tobytes()
+    path = tmp_path / "x.wav"
+    path.write_bytes(_wav_bytes(channels, width, 44100, raw))
+    _, pcm = ingest.read_wav(path, quirk=quirk)
+    nb = (frames + block - 1) // block
+    seen = 0
+    for first, rows, bits, tail_len, n_tail in ingest.iter_wav_batches(path, block, per, quirk):
+        assert first == seen
+        want_rows, _, want_tail, want_nt = ingest.planar_blocks(pcm, block, first, per)
+        assert np.array_equal(rows.astype(np.int64), want_rows.astype(np.int64))
+        assert (tail_len, n_tail) == (want_tail, want_nt)
+        seen += rows.shape[0] // channels
+    assert seen == nb
+
+
+def test_cli_reader_error_after_stream_header(tmp_path):
+    """The reference CLI raises its reader's IndexError (encoder.py:102) after writing the
+    42-byte stream header; so does ours (before touching a device)."""
+    from flac_amd import cli
+    path = tmp_path / "x.wav"
+    path.write_bytes(_wav_bytes(3, 2, 44100, bytes(range(60)) * 10))
+    out = tmp_path / "x.flac"
+    with pytest.raises(IndexError):
+        cli.main(["encode", str(path), str(out)])
+    data = out.read_bytes()
+    assert len(data) == 42 and data[:4] == b"fLaC"
 
 
 def _sine(n):
