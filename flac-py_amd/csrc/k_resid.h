@@ -664,8 +664,13 @@ __device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta
  *   kVarList     unit = retry_list[blockIdx.x] for blockIdx.x < *retry_count, every path. */
 enum { kVarGeneric = 0, kVarFast = 1, kVarList = 2 };
 template <int LMAX, int PATH, typename ResT, int VAR>
-__device__ __forceinline__ void k_resid_body(const ResidArgs& a, const int64_t gid) {
+__global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArgs a) {
     constexpr bool FAST = VAR == kVarFast;
+    int64_t gid = blockIdx.x;
+    if constexpr (VAR == kVarList) {
+        if (gid >= (int64_t)*a.retry_count) return;
+        gid = a.retry_list[gid];
+    }
     using UX = ResT;
     constexpr bool S16 = PATH == PATH_S16;
     constexpr bool WIDE = PATH == PATH_W64 || PATH == PATH_W64S;
@@ -1456,24 +1461,6 @@ __device__ __forceinline__ void k_resid_body(const ResidArgs& a, const int64_t g
     } /* !FAST */
 }
 
-/* kVarGeneric / kVarFast: unit = blockIdx.x.  kVarList: a bounded grid loops over the listed
- * units (the list's length is only known on the device); the barrier in front of each unit
- * keeps a unit's LDS staging behind every wave of the previous one. */
-template <int LMAX, int PATH, typename ResT, int VAR>
-__global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArgs a) {
-    if constexpr (VAR == kVarList) {
-        const int64_t cnt = (int64_t)*a.retry_count;
-        for (int64_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-            __syncthreads();
-            k_resid_body<LMAX, PATH, ResT, VAR>(a, a.retry_list[i]);
-        }
-    } else {
-        k_resid_body<LMAX, PATH, ResT, VAR>(a, (int64_t)blockIdx.x);
-    }
-}
-
-/* grid of the list variant: enough workgroups to fill the chip when many units are listed */
-constexpr int64_t kListGrid = 2048;
 
 template <int LMAX, int PATH, typename ResT>
 static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
@@ -1513,7 +1500,7 @@ static hipError_t launch_resid_fast(const ResidArgs& a, hipStream_t s) {
     auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
     e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gen);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kl, dim3((unsigned)(a.count < kListGrid ? a.count : kListGrid)), dim3(nt), lds_gen, s, a);
+    hipLaunchKernelGGL(kl, dim3((unsigned)a.count), dim3(nt), lds_gen, s, a);
     return hipGetLastError();
 }
 
@@ -1529,7 +1516,7 @@ static hipError_t launch_resid_list(const ResidArgs& a, hipStream_t s) {
     auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
     hipError_t e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kl, dim3((unsigned)(a.count < kListGrid ? a.count : kListGrid)), dim3(nt), lds, s, a);
+    hipLaunchKernelGGL(kl, dim3((unsigned)a.count), dim3(nt), lds, s, a);
     return hipGetLastError();
 }
 

@@ -50,8 +50,14 @@ constexpr int kCoefLimit = 127;              /* (sum|c| + 2^shift) * 33023 < 2^2
 constexpr int kRiceOrders = 8;               /* orders 0..7 kept per finest partition */
 
 struct SLds {
-    int xs, rec, red, red0, red2, cs, pk, mst, misc, total;
+    int xs, rec, red, red0, red2, pks, pk, tap, bnd, mst, total;
 };
+
+/* MFMA tap table: 16 predictor columns (4 groups x 4 orders) x kTapN entries idx in
+ * [-2, 16); entry idx holds the f16 pair (T[idx], T[idx-1]) where T[0] is the x[i] tap and
+ * T[m+1] the coefficient of x[i-1-m] (0 outside the predictor), once plain (L: low sample
+ * bytes) and once times 256 (H: high bytes). */
+constexpr int kTapN = 18;
 
 __host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P) {
     auto up = [](int b) { return (b + 15) & ~15; };
@@ -62,10 +68,11 @@ __host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P) 
     l.red = o;  o = up(o + 4 * nw * 64);            /* u32 [nw][group][order][kb] */
     l.red0 = o; o = up(o + 4 * nw);                 /* u32 [nw] sum|x| */
     l.red2 = o; o = up(o + 8 * (nw + 1) * kRiceOrders); /* u64 [nw][order] data bits, [order] headers */
-    l.cs = o;   o = up(o + 4 * (n / 8));            /* u32 chunk sums of the chosen residual */
-    l.pk = o;   o = up(o + nw * P * 4 * kRiceOrders); /* u32 [nw][P][order] = p | p << 16 */
-    l.mst = o;  o = up(o + 4 * 20);                  /* wave 0: meta scalar fields */
-    l.misc = o; o = up(o + 4 * 4);                   /* Rice error key / site, Rice5Bit order mask */
+    l.pks = o;  o = up(o + 4 * P);                  /* u32 finest partition sums */
+    l.pk = o;   o = up(o + P * 4 * kRiceOrders);    /* u32 [P][order] = p | p << 16 (every wave writes the same) */
+    l.tap = o;  o = up(o + 2 * 16 * kTapN * 4);     /* u32 [H|L][16 columns][kTapN] f16 pairs */
+    l.bnd = o;  o = up(o + 4 * 16);                 /* per LPC order: outside the MFMA exactness bound */
+    l.mst = o;  o = up(o + 4 * 20);                 /* wave 0: meta scalar fields */
     l.total = o;
     return l;
 }
@@ -215,8 +222,10 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
     uint32_t* red = reinterpret_cast<uint32_t*>(smem + lay.red);
     uint32_t* red0 = reinterpret_cast<uint32_t*>(smem + lay.red0);
     unsigned long long* red2 = reinterpret_cast<unsigned long long*>(smem + lay.red2);
-    uint32_t* pks = reinterpret_cast<uint32_t*>(smem + lay.cs);  /* finest partition sums */
-    uint32_t* pkw = reinterpret_cast<uint32_t*>(smem + lay.pk) + wid * Pmax * kRiceOrders;
+    uint32_t* pks = reinterpret_cast<uint32_t*>(smem + lay.pks); /* finest partition sums */
+    uint32_t* pkw = reinterpret_cast<uint32_t*>(smem + lay.pk);
+    uint32_t* tap = reinterpret_cast<uint32_t*>(smem + lay.tap);
+    int* bnd = reinterpret_cast<int*>(smem + lay.bnd);
     uint32_t* mst = reinterpret_cast<uint32_t*>(smem + lay.mst);
     flacmi_unit_meta* meta = a.meta + gid;
     MetaVals mv{};
@@ -262,6 +271,55 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         if (lane == 0) red0[wid] = sx;
     }
     __syncthreads(); /* B1 */
+    /* the MFMA tap table (and, per LPC order, the exactness bound) from the staged record */
+    {
+        const int32_t* rg = recl;
+        for (int e = tid; e < 4 * (NG + 1) * kTapN; e += NT) {
+            const int col = e / kTapN, idx = e - col * kTapN - 2, g = col >> 2, o4 = col & 3;
+            int p = o4 + 1, sh = 0;
+            const int32_t* cp = rg;
+            bool live = true;
+            if (g > 0) {
+                p = 4 * (g - 1) + o4 + 1;
+                live = NG > 0 && p <= L;
+                if (live) {
+                    sh = rg[2 + p - 1];
+                    cp = rg + 2 + L + (p * (p - 1)) / 2;
+                }
+            }
+            float t2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ix = idx - h;
+                float v = 0.0f;
+                if (live && ix == 0) {
+                    v = g == 0 ? -1.0f : -(float)(1 << sh);
+                } else if (live && ix >= 1 && ix <= p) {
+                    const int m = ix - 1;
+                    if (g == 0) { /* fixed order p (common.py:15-21): x[i-1-m] weighs (-1)^m C(p, m+1) */
+                        const int c1 = p, c2 = p * (p - 1) / 2, c3 = p * (p - 1) * (p - 2) / 6,
+                                  c4 = p * (p - 1) * (p - 2) * (p - 3) / 24;
+                        v = (float)(m == 0 ? c1 : m == 1 ? -c2 : m == 2 ? c3 : -c4);
+                    } else {
+                        v = (float)cp[m];
+                    }
+                }
+                t2[h] = v;
+            }
+            tap[col * kTapN + idx + 2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t2[0], 256.0f * t2[1]));
+            tap[(16 + col) * kTapN + idx + 2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t2[0], t2[1]));
+            if (NG > 0 && g > 0 && idx == 0 && live) { /* (sum|c| + 2^shift) * 33023 < 2^22 */
+                int c[4 * (NG > 0 ? NG : 1)];
+#pragma unroll
+                for (int m = 0; m < 4 * (NG > 0 ? NG : 1); ++m) c[m] = m < p ? cp[m] : 0; /* independent reads */
+                int sa = 1 << sh;
+#pragma unroll
+                for (int m = 0; m < 4 * (NG > 0 ? NG : 1); ++m) sa += c[m] < 0 ? -c[m] : c[m];
+                bnd[p - 1] = sa > kCoefLimit;
+            }
+        }
+    }
+    __syncthreads(); /* B1b: tap table */
 
     /* ---- unit status from the LPC record; MFMA exactness bound per order ---- */
     uint32_t negmask = 0;
@@ -276,18 +334,7 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
             return;
         }
         negmask = (uint32_t)recl[1];
-        int sa = 0;
-        if (lane < L) {
-            const int p = lane + 1;
-            const int32_t* cp = recl + 2 + L + (p * (p - 1)) / 2;
-            int c[4 * NG];
-#pragma unroll
-            for (int j = 0; j < 4 * NG; ++j) c[j] = j < p ? cp[j] : 0; /* independent reads */
-            sa = 1 << recl[2 + lane];
-#pragma unroll
-            for (int j = 0; j < 4 * NG; ++j) sa += c[j] < 0 ? -c[j] : c[j];
-        }
-        if (__ballot(sa > kCoefLimit)) { /* outside the exactness bound: k_resid redoes it */
+        if (__ballot(lane < L && bnd[lane < L ? lane : 0])) { /* outside the exactness bound: k_resid redoes it */
             if (tid == 0) {
                 meta->status = FLACMI_STATUS_RETRY;
                 const unsigned long long k = atomicAdd(a.retry_count, 1ull);
@@ -304,51 +351,18 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         h8 B[NG + 1];
         int shg[NG + 1], startg[NG + 1];
         uint32_t kg[NG + 1];
+        const int idx0 = 12 + rho - 4 * kb + 2; /* table position of tap jj = 0 */
 #pragma unroll
         for (int g = 0; g <= NG; ++g) {
-            int p = 0, sh = 0, start = 0;
-            const int32_t* cp = recl;
-            if (g == 0) {
-                p = o4 + 1; /* fixed order */
-                start = p;
-            } else {
-                p = 4 * (g - 1) + o4 + 1; /* LPC order */
-                if (p <= L) {
-                    sh = recl[2 + p - 1];
-                    cp = recl + 2 + L + (p * (p - 1)) / 2;
-                    start = ((negmask >> (p - 1)) & 1) ? 0 : p;
-                } else {
-                    p = 0;
-                }
+            const uint32_t* th = tap + (4 * g + o4) * kTapN;
+            const uint32_t* tl = tap + (16 + 4 * g + o4) * kTapN;
+            B[g] = __builtin_bit_cast(h8, uint4{th[idx0], th[idx0 - 2], tl[idx0], tl[idx0 - 2]});
+            int sh = 0, start = o4 + 1;
+            if (g > 0) {
+                const int p = 4 * (g - 1) + o4 + 1;
+                sh = p <= L ? recl[2 + p - 1] : 0;
+                start = ((negmask >> (p - 1)) & 1) ? 0 : p;
             }
-            float t[4];
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const int d = 4 * kb + jj - 12 - rho; /* tap offset: x[i + d] */
-                const int m = -d - 1;
-                float v = 0.0f;
-                if (g == 0) {
-                    /* fixed order k (common.py:15-21): x[i-1-m] weighs (-1)^m C(k, m+1) */
-                    const int k = p;
-                    if (d == 0) {
-                        v = -1.0f;
-                    } else if (m >= 0 && m < k) {
-                        const int c1 = k, c2 = k * (k - 1) / 2, c3 = k * (k - 1) * (k - 2) / 6,
-                                  c4 = k * (k - 1) * (k - 2) * (k - 3) / 24;
-                        v = (float)(m == 0 ? c1 : m == 1 ? -c2 : m == 2 ? c3 : -c4);
-                    }
-                } else if (p > 0) {
-                    if (d == 0) v = -(float)(1 << sh);
-                    else if (m >= 0 && m < p) v = (float)cp[m];
-                }
-                t[jj] = v;
-            }
-            uint32_t w[4];
-            w[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[0], 256.0f * t[1]));
-            w[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[2], 256.0f * t[3]));
-            w[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t[0], t[1]));
-            w[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t[2], t[3]));
-            B[g] = __builtin_bit_cast(h8, uint4{w[0], w[1], w[2], w[3]});
             shg[g] = sh;
             kg[g] = kMagicBits >> sh;
             startg[g] = start;
@@ -455,13 +469,13 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         lpc_wins = lsum < fsum;
         tie = !lpc_wins && !(fsum < lsum);
     }
-    if (wid == 0) {
+    if (wid == 0 && a.fixed_sums) {
         const uint64_t fv = (uint64_t)__shfl((unsigned long long)tj, lane == 0 ? 16 : (lane - 1) & 63);
-        if (a.fixed_sums && lane < 5) a.fixed_sums[gid * 5 + lane] = (long long)fv;
-        if (a.lpc_sums && lane < 32) {
-            const uint64_t v = (uint64_t)__shfl((unsigned long long)tj, (lane + 4) & 63);
-            a.lpc_sums[gid * 32 + lane] = (lane + 1 <= L) ? (long long)v : 0;
-        }
+        if (lane < 5) a.fixed_sums[gid * 5 + lane] = (long long)fv;
+    }
+    if (wid == 0 && a.lpc_sums) {
+        const uint64_t v = (uint64_t)__shfl((unsigned long long)tj, (lane + 4) & 63);
+        if (lane < 32) a.lpc_sums[gid * 32 + lane] = (lane + 1 <= L) ? (long long)v : 0;
     }
     mv.fixed_order = fo;
     mv.lpc_order = lbest;

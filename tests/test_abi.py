@@ -90,3 +90,29 @@ def test_decode_golden_covers_every_reference_exception_site():
     for must in ("constant_192", "verbatim_256", "fixed2_wasted2", "lpc32_p15", "stereo_M_S",
                  "lpc6_rice5_escape_bs16", "fixed3_32bit"):
         assert must in names
+
+
+def test_no_kernel_spills_to_scratch():
+    """Every kernel in libflacmi.so fits its registers: the Makefile keeps the compiler's
+    per-kernel resource report next to each object, and a scratch (spill) size other than 0
+    is a several-fold slowdown that no parity test notices (round-2 regression: the generic
+    k_resid grew from 75 VGPRs to 256 + 692 B/lane of scratch when its body moved into an
+    inlined helper)."""
+    import glob
+    import pytest
+    build = os.path.join(os.path.dirname(LIB_PATH), "csrc", "build")
+    reports = sorted(glob.glob(os.path.join(build, "*.res")))
+    if not reports:
+        pytest.skip("no resource reports (library built elsewhere)")
+    spills, kernels = [], 0
+    for rep in reports:
+        name = None
+        for line in open(rep):
+            m = re.search(r"Function Name: (\S+)", line)
+            if m:
+                name, kernels = m.group(1), kernels + 1
+            m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+            if m and int(m.group(1)):
+                spills.append((os.path.basename(rep), name, int(m.group(1))))
+    assert kernels >= 40, f"only {kernels} kernels reported"
+    assert not spills, f"kernels spilling to scratch: {spills}"

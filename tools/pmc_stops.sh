@@ -1,0 +1,10 @@
+# Instruction counts per k_resid_stream phase: one rocprofv3 --pmc pass per ablation stop.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/${1:-pmcstops}; shift
+mkdir -p $OUT
+ARGS="--units 200000 --steps 2 --warmup 1 --cpu-seconds 0 --no-parity --no-frames $*"
+for k in 1 2 3 4 0; do
+  FLACMI_DEBUG_STOP=$k timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_MFMA --output-format csv -d $OUT/s$k -o run -- python3 bench.py $ARGS > $OUT/s$k.json 2> $OUT/s$k.err || { echo "stop $k failed"; tail -5 $OUT/s$k.err; exit 1; }
+  echo "== stop $k"; python3 tools/pmc_summary.py $OUT/s$k | grep -A9 k_resid_stream
+done
