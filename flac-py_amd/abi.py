@@ -209,4 +209,6 @@ SIGNATURES = {
     "flacmi_host_floor_log2": (C.c_int32, [C.c_double]),
     "flacmi_device_selftest": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                                          C.c_int64]),
+    "flacmi_device_lpc_from_acf": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
+                                             C.c_void_p]),
 }

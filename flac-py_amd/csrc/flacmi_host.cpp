@@ -998,4 +998,32 @@ int flacmi_device_selftest(flacmi_ctx* ctx, int32_t which, const double* x, doub
     return rc;
 }
 
+int flacmi_device_lpc_from_acf(flacmi_ctx* ctx, const double* acf, int64_t n, int32_t L, int32_t q, int32_t* rec) {
+    if (!ctx || !acf || !rec) return fail(FLACMI_E_INVALID, "null argument");
+    if (L < 1 || L > FLACMI_MAX_LPC_ORDER) return fail(FLACMI_E_INVALID, "L must be in 1..%d", FLACMI_MAX_LPC_ORDER);
+    if (q < 5 || q > 15) return fail(FLACMI_E_INVALID, "q must be in 5..15");
+    if (n <= 0) return 0;
+    if (int rc = set_device(ctx)) return rc;
+    const int rw = FLACMI_LPC_REC_WORDS(L);
+    void* d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)n * (33 * 8 + (size_t)rw * 4)));
+    LpcArgs a{};
+    a.acf = (double*)d;
+    a.rec = (int32_t*)(a.acf + n * 33);
+    a.count = n;
+    a.n = 1 << 12;
+    a.L = L;
+    a.q = q;
+    a.rec_words = rw;
+    a.log2thr = ctx->d_log2thr;
+    int rc = 0;
+    hipError_t e = hipMemcpyAsync(a.acf, acf, (size_t)n * 33 * 8, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = launch_lpc_from_acf(a, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(rec, a.rec, (size_t)n * rw * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) rc = fail(FLACMI_E_HIP, "lpc_from_acf: %s", hipGetErrorString(e));
+    (void)hipFree(d);
+    return rc;
+}
+
 }  // extern "C"

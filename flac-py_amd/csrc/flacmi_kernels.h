@@ -118,6 +118,8 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes);
 constexpr int kMaxFinestParts = 4096;
 
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);
+/* k_lpc<32> with the autocorrelation read from a.acf (flacmi_device_lpc_from_acf) */
+hipError_t launch_lpc_from_acf(const LpcArgs& a, hipStream_t s);
 /* path: 0 = int16 samples / sdot2, 1 = int32 samples / mad24, 2 = int64 arithmetic */
 hipError_t launch_resid(const ResidArgs& a, int path, int residual_bytes, hipStream_t s);
 hipError_t launch_expand_records(const int32_t* rec, int32_t rec_words, int32_t L, int64_t count,

@@ -18,7 +18,10 @@ __device__ __forceinline__ void write_quant(int32_t* rec, int L, int p, const in
         if (j < p) c[j] = j < nq ? q[j] : 0;
 }
 
-template <int LMAX, typename SampleT>
+/* ACF_IN: the autocorrelation is read from a.acf ([count][33]) instead of computed from
+ * samples -- the entry point flacmi_device_lpc_from_acf uses to drive Levinson-Durbin and
+ * the quantiser into the overflow sites integer PCM never reaches. */
+template <int LMAX, typename SampleT, bool ACF_IN = false>
 __global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
     const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (gid >= a.count) return;
@@ -27,6 +30,12 @@ __global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
     int32_t* __restrict__ rec = a.rec + gid * a.rec_words;
     const int n = a.n, L = a.L, q = a.q;
 
+    constexpr int S = ((LMAX + 1 + 7) / 8) * 8;
+    double acc[LMAX + 1];
+    if constexpr (ACF_IN) {
+#pragma unroll
+        for (int l = 0; l <= LMAX; ++l) acc[l] = l <= L ? a.acf[gid * 33 + l] : 0.0;
+    } else {
     if (n >= 4 && n <= 7) { /* tukey: nr == 0 -> pi * 0 / 0 (encoder.py:437) */
         rec[0] = ST_ZERODIV | (FLACMI_SITE_TUKEY << 16);
         rec[1] = 0;
@@ -36,9 +45,7 @@ __global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
     }
 
     /* ---- autocorrelation: acc[l] = sum_{m} a[m-l] * a[m], m = 0 .. n-2 ---- */
-    constexpr int S = ((LMAX + 1 + 7) / 8) * 8;
     double ring[S];
-    double acc[LMAX + 1];
 #pragma unroll
     for (int t = 0; t < S; ++t) ring[t] = 0.0;
 #pragma unroll
@@ -122,6 +129,7 @@ __global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
 #pragma unroll
         for (int l = 0; l < 33; ++l) o[l] = (l <= LMAX && l <= L) ? acc[l < LMAX ? l : LMAX] : 0.0;
     }
+    } /* !ACF_IN */
 
     /* ---- Levinson-Durbin at max order with a snapshot per order (encoder.py:453-479) ---- */
     const pym::PowTables PT{c_log_hdr, c_log_tab, c_exp_hdr, c_exp_tab};
@@ -235,6 +243,12 @@ static hipError_t launch_lpc_T(const LpcArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((k_lpc<LMAX, int16_t>), grid, dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL((k_lpc<LMAX, int32_t>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_lpc_from_acf(const LpcArgs& a, hipStream_t s) {
+    if (a.count <= 0) return hipSuccess;
+    hipLaunchKernelGGL((k_lpc<32, int32_t, true>), dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

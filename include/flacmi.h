@@ -342,6 +342,14 @@ int32_t flacmi_host_floor_log2(double x);
  * which = 1: out[i] = floor(log2(x[i])) for finite x[i] > 0. */
 int flacmi_device_selftest(flacmi_ctx* ctx, int32_t which, const double* x, double* out,
                            int32_t* status, int64_t n);
+/* k_lpc's Levinson-Durbin + quantiser (encoder.py:453-534) driven from n autocorrelation
+ * rows acf[n][33] (lags 0..L used) instead of samples: rec[n][FLACMI_LPC_REC_WORDS(L)]
+ * receives the LPC record k_lpc writes (word 0 = status | site << 16, word 1 = negative-shift
+ * mask, then L shifts and the triangular coefficient table).  Reaches the overflow sites
+ * (FLACMI_SITE_LEVINSON_POW, FLACMI_SITE_QUANT_LOG2) that no integer PCM block reaches
+ * (DESIGN §4).  Synchronous; L in 1..32, q in 5..15. */
+int flacmi_device_lpc_from_acf(flacmi_ctx* ctx, const double* acf, int64_t n, int32_t L, int32_t q,
+                               int32_t* rec);
 
 #ifdef __cplusplus
 }

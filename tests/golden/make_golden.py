@@ -357,6 +357,74 @@ def stream_set():
     return out
 
 
+# ---------------------------------------------------------------------------------
+# ACF-driven rows: the Levinson-Durbin / quantiser exception sites that integer PCM
+# never reaches (encoder.py:476 OverflowError of lambda_ ** 2, encoder.py:503
+# floor(log2(inf))), reached from autocorrelation vectors directly.  Each row runs the
+# reference's steps 3-4 of encode_subframe_lpc (encoder.py:376-384) on the row: every
+# order's levinson_durbin first, then every order's quantize_lpc_coefficients.
+# ---------------------------------------------------------------------------------
+def _raise_line(e):
+    import traceback
+    tb = [f for f in traceback.extract_tb(e.__traceback__) if f.filename.endswith("encoder.py")]
+    return tb[-1].lineno if tb else None
+
+
+def ref_from_acf(ac, L, q):
+    out = {"acf": [float(a).hex() for a in ac], "L": L, "q": q}
+    try:
+        coefs = [E.levinson_durbin(ac[:i]) for i in range(2, L + 2)]
+    except Exception as e:
+        out["exception"] = dict(exc(e), stage="levinson", line=_raise_line(e))
+        return out
+    out["levinson"] = [[x.hex() for x in c] for c in coefs]
+    quants = []
+    for c in coefs:
+        try:
+            qc, sh = E.quantize_lpc_coefficients(c, q)
+        except Exception as e:
+            out["exception"] = dict(exc(e), stage="quant", line=_raise_line(e), order=len(c))
+            break
+        quants.append({"coefs": qc, "shift": sh})
+    out["quant"] = quants
+    return out
+
+
+def acf_set():
+    rows = []
+    tiny = 5e-324
+    # lambda_ ** 2 overflows at the first / a later step (encoder.py:476)
+    for L, q, ac in ((1, 5, [1e-200, 1.0]), (4, 12, [1e-160, -3.0, 2.0, 1.0, 0.5]),
+                     (8, 15, [1.0, 0.5, 0.25, 0.125, 1e200, 0.0, 0.0, 0.0, 0.0]),
+                     (32, 5, [1e-300] + [1e10 / (k + 1) for k in range(32)])):
+        rows.append(ref_from_acf(ac, L, q))
+    # lambda_ overflows to inf in the division (no exception), coefficient inf -> floor(log2(inf))
+    for L, q, ac in ((1, 5, [tiny, 1.0]), (2, 5, [1e-310, 1.0, 1.0]), (12, 15, [tiny] + [1.0] * 12)):
+        rows.append(ref_from_acf(ac, L, q))
+    # zero error, assertion sites, NaN coefficients
+    for L, q, ac in ((3, 5, [0.0, 1.0, 1.0, 1.0]), (2, 5, [1.0, 0.0, 0.0]), (2, 5, [1e-30, 1.0, 0.3]),
+                     (2, 5, [1.0, float("nan"), 0.0]), (2, 5, [1.0, 0.5, float("nan")]),
+                     (3, 5, [float("inf"), 1.0, 1.0, 1.0]), (2, 5, [1.0, float("inf"), 0.0])):
+        rows.append(ref_from_acf(ac, L, q))
+    # random rows over a wide exponent range: one row per distinct outcome
+    rnd = random.Random(4711)
+    found = {}
+    for trial in range(20000):
+        L = rnd.choice([1, 2, 3, 4, 8, 12, 32])
+        q = rnd.choice([5, 12, 15])
+        ac = [rnd.choice([-1, 1]) * 10.0 ** rnd.uniform(-320, 300) if rnd.random() < 0.3 else
+              rnd.uniform(-1, 1) * 10.0 ** rnd.uniform(-5, 5) for _ in range(L + 1)]
+        ac[0] = abs(ac[0])
+        r = ref_from_acf(ac, L, q)
+        ex = r.get("exception")
+        key = (ex["type"], ex["stage"], ex["line"]) if ex else ("ok", min(L, 4))
+        if found.get(key, 0) < 3:
+            found[key] = found.get(key, 0) + 1
+            rows.append(r)
+    print("acf outcomes:", sorted(str(k) for k in found), flush=True)
+    return rows
+
+
 def dump(name, obj):
     path = os.path.join(OUT, name)
     with open(path, "w") as f:
@@ -382,7 +450,10 @@ def main(which):
         dump("edge.json", {"config": "edge cases and reference exceptions", "units": edge_set()})
     if "stream" in which:
         dump("streams.json", stream_set())
+    if "acf" in which:
+        dump("acf_sites.json", {"config": "Levinson-Durbin / quantiser sites driven from ACF rows",
+                                "rows": acf_set()})
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["c2", "c1", "c3", "c5", "edge", "stream"])
+    main(sys.argv[1:] or ["c2", "c1", "c3", "c5", "edge", "stream", "acf"])

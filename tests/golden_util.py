@@ -120,3 +120,43 @@ def check(res, entry, intermediates=True):
     eq("rice_bits", int(res["rice_bits"]), exp["rice_bits"])
     eq("zz_sha256", zz_sha(res["residual"]), exp["zz_sha256"])
     return bad
+
+
+# reference raise line (encoder.py) -> flacmi_site, for the ACF-driven rows (acf_sites.json)
+ACF_LINE_SITE = {469: 2, 476: 3, 496: 4, 503: 5, 508: 6}
+
+
+def acf_expected_site(exc):
+    """flacmi_site of a reference exception recorded by make_golden.ref_from_acf."""
+    if exc["line"] in (520, 530):
+        return 7 if exc["type"] == "OverflowError" else 8
+    return ACF_LINE_SITE[exc["line"]]
+
+
+def acf_rows():
+    d = load("acf_sites.json")
+    for r in d["rows"]:
+        r = dict(r)
+        r["acf_values"] = [float.fromhex(h) for h in r["acf"]]
+        yield r
+
+
+def check_acf_record(rec, row):
+    """Mismatches between an LPC record (k_lpc layout for L = row['L']: word 0 status|site<<16,
+    word 1 negative-shift mask, L shifts, triangular coefficients) and a reference row."""
+    L, bad = row["L"], []
+    exc = row.get("exception")
+    st, site = int(rec[0]) & 0xFFFF, int(rec[0]) >> 16
+    if exc:
+        if (st, site) != (EXC_STATUS[exc["type"]], acf_expected_site(exc)):
+            bad.append(f"status/site {(st, site)} want {(EXC_STATUS[exc['type']], acf_expected_site(exc))} {exc}")
+    elif (st, site) != (0, 0):
+        bad.append(f"status/site {(st, site)} want ok")
+    for o, q in enumerate(row.get("quant", []), start=1):
+        neg = (int(rec[1]) >> (o - 1)) & 1
+        ncoef = 0 if neg else o
+        base = 2 + L + (o * (o - 1)) // 2
+        got = ([int(v) for v in rec[base: base + ncoef]], int(rec[2 + o - 1]))
+        if got != (q["coefs"], q["shift"]):
+            bad.append(f"order {o}: got {got} want {(q['coefs'], q['shift'])}")
+    return bad

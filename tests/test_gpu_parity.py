@@ -189,6 +189,30 @@ def test_device_pypow2_and_floor_log2_match_libm(az):
         assert int(got2[i]) == oracle.floor_log2(float(pos[i]))[0]
 
 
+def test_device_lpc_sites_from_acf_rows(az):
+    """k_lpc's Levinson-Durbin + quantiser driven from ACF rows (flacmi_device_lpc_from_acf)
+    against the reference's outcome on the same rows (tests/golden/acf_sites.json): the
+    OverflowError sites encoder.py:476 (lambda_ ** 2) and :503 (floor(log2(inf))) that no
+    integer PCM block reaches, plus the other Levinson/quantiser outcomes."""
+    from collections import defaultdict
+    groups = defaultdict(list)
+    for row in G.acf_rows():
+        groups[(row["L"], row["q"])].append(row)
+    sites, bad = set(), []
+    for (L, q), rows in groups.items():
+        acf = np.zeros((len(rows), 33), dtype=np.float64)
+        for i, r in enumerate(rows):
+            acf[i, : L + 1] = r["acf_values"]
+        rec = np.zeros((len(rows), abi.lpc_rec_words(L)), dtype=np.int32)
+        assert az.lib.flacmi_device_lpc_from_acf(az.ctx, acf.ctypes.data, len(rows), L, q, rec.ctypes.data) == 0
+        for i, r in enumerate(rows):
+            bad += [f"L={L} q={q} row {i}: {m}" for m in G.check_acf_record(rec[i], r)]
+            if r.get("exception"):
+                sites.add(int(rec[i, 0]) >> 16)
+    assert not bad, "\n".join(bad[:20])
+    assert {3, 5} <= sites, sites
+
+
 def test_synth_device_matches_oracle(az):
     import ctypes as C
     n_units, n = 9, 4608

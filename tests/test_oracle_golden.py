@@ -46,3 +46,39 @@ def test_levinson_snapshots_equal_per_order_runs():
         for o, want in enumerate(e["expect"]["inter"]["levinson"], start=1):
             st, site, c = oracle.levinson(acf, o)
             assert [v.hex() for v in c] == want
+
+
+def test_oracle_levinson_quantize_on_acf_rows():
+    """The overflow sites integer PCM never reaches: the oracle's Levinson and
+    quantiser, run as encode_subframe_lpc runs them (every order's Levinson, then every
+    order's quantisation, encoder.py:376-384), against the reference on ACF rows
+    (tests/golden/acf_sites.json)."""
+    sites = set()
+    for row in G.acf_rows():
+        L, q, ac = row["L"], row["q"], row["acf_values"]
+        exc = row.get("exception")
+        got = None
+        coefs = []
+        for o in range(1, L + 1):
+            st, site, c = oracle.levinson(ac[: o + 1], o)
+            if st:
+                got = (st, site)
+                break
+            coefs.append(c)
+        quant = []
+        if got is None:
+            for c in coefs:
+                st, site, qc, sh = oracle.quantize(c, q)
+                if st:
+                    got = (st, site)
+                    break
+                quant.append({"coefs": [int(v) for v in qc], "shift": sh})
+            if exc is None:
+                assert [[v.hex() for v in c] for c in coefs] == row["levinson"]
+        if exc:
+            assert got == (G.EXC_STATUS[exc["type"]], G.acf_expected_site(exc)), (row, got)
+            sites.add(got[1])
+        else:
+            assert got is None, (row, got)
+        assert quant == row.get("quant", []), row
+    assert {3, 5} <= sites, sites
