@@ -1,20 +1,17 @@
 /* k_stream.hip — the residual-side analysis (candidate sums, choice, chosen residual, Rice
- * search) for the common 16-bit shapes as a PERSISTENT, software-pipelined kernel.
+ * search) for the common 16-bit shapes: k_resid_stream, one workgroup per unit.
  *
- * Same results as k_resid (k_resid.h) bit for bit; it replaces k_resid's one-workgroup-per-
- * unit launch where the shape allows (host check: stream_shape_ok):
- *   int16 samples, q <= 16, 32-bit residual rows, reference mode with 1 <= L <= 12 or
- *   fixed-only mode, n % 64 == 0, 64 <= n <= 6144, finest Rice partitions of whole
- *   8-sample chunks, at most 64 of them.
+ * Same results as k_resid (k_resid.h) bit for bit; it replaces k_resid's launch where the
+ * shape allows (host check: stream_shape_ok):
+ *   int16 samples, 32-bit residual rows, reference mode with 1 <= L <= 12 or fixed-only
+ *   mode, n % 64 == 0, 64 <= n <= 6144, at most 32 finest Rice partitions of whole
+ *   8-sample chunks.
  *
  * Reference semantics (flac/encoder.py): fixed predictors 331-359, LPC candidate residuals
  * 386-404 with prediction_residual 537-548, the fixed-vs-LPC choice 133-157, encode_residual
  * + rice_partitions + find_rice_parameter + rice_size 632-760.
  *
- * Structure (one workgroup of nw = n/1536 rounded-up waves, looping over units
- * u = blockIdx.x, += gridDim.x; grid = resident workgroups):
- *   - the NEXT unit's samples and LPC record are loaded into registers right after the
- *     current unit is staged, so HBM latency hides behind a whole unit of compute;
+ * Structure (nw = n/1536 rounded-up waves per workgroup, four workgroup barriers):
  *   - samples sit in LDS biased (x ^ 0x8000: unsigned 16-bit), which makes the MFMA operand
  *     build two byte permutes and two packed subtracts per lane and block;
  *   - candidate sums on v_mfma_f32_16x16x32_f16 with INTEGER taps and the accumulator
@@ -25,12 +22,15 @@
  *     (bits >> shift) - (0x4B400000 >> shift) = floor(T / 2^shift) = -r exactly.  Fixed
  *     predictors (shift 0): |r| is one v_sad_u32; LPC: one shift + one v_sad_u32.
  *     MFMA 0 holds fixed orders 1..4 x 4 sample phases, MFMAs 1..NG the LPC orders
- *     4(g-1)+1 .. 4g x 4 phases.  Units outside the bound are listed for k_resid.
- *   - the choice, the Rice parameters (per-wave butterfly over the finest partitions) and
- *     the order choice are computed redundantly by every wave from LDS data, so a unit
- *     needs four workgroup barriers and no single-wave serial section;
- *   - Rice data bits on packed 16-bit pairs (v_pk_lshrrev_b16 + v_dot2_u32_u16) when a
- *     chunk's values are < 2^16;
+ *     4(g-1)+1 .. 4g x 4 phases, from a tap table built once per unit in LDS.  Units
+ *     outside the bound are listed for k_resid;
+ *   - the choice (a lane-parallel DPP argmin), the Rice parameters (one heap node per lane,
+ *     finest partition sums by LDS atomics) and the order choice are
+ *     computed redundantly by every wave from LDS data, so no single-wave serial section
+ *     sits between barriers;
+ *   - the chosen residual is written to HBM from registers and kept as packed 16-bit pairs;
+ *     Rice data bits on those pairs (v_pk_lshrrev_b16 + v_dot2_u32_u16) when a chunk's
+ *     values are < 2^16;
  *   - the 208-byte meta record is one coalesced store of 52 lanes.
  */
 #include "device_common.h"
@@ -81,6 +81,14 @@ __host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P) 
  * constant b there).  Not inline asm: the hazard recognizer does not see an asm operand
  * read an MFMA result, and such a read without the required wait states returns garbage. */
 __device__ __forceinline__ uint32_t sad32(uint32_t a, uint32_t b, uint32_t acc) { return (a > b ? a - b : b - a) + acc; }
+/* min with the DPP-moved value of a u64 (all lanes of a row valid for the row patterns used) */
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_min_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xf, 0xf, false);
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    return o < v ? o : v;
+}
 __device__ __forceinline__ uint32_t opaque(uint32_t v) {
     asm volatile("" : "+v"(v));
     return v;
@@ -420,61 +428,59 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
     __syncthreads(); /* B2 */
     if (a.stop_after == 2) return;
 
-    /* ---- choice (encoder.py:331-359, 398-404, 135-157), every wave ----
-     * lane j < 4: fixed order j+1; 4 <= j < 16: LPC order j-3; lane 16: fixed order 0 */
+    /* ---- choice (encoder.py:331-359, 398-404, 135-157), every wave, lane-parallel ----
+     * lanes 0..4: fixed orders 0..4; lanes 16..15+L: LPC orders 1..L.  Key = sum * 16 + index,
+     * so a row's minimum key is its smallest sum at the lowest order (python min(): the first
+     * minimum); four DPP steps reduce each 16-lane row. */
     uint64_t tj = 0;
-    if (lane < 4 * (NG + 1)) {
-#pragma unroll 1
-        for (int w2 = 0; w2 < nw; ++w2) {
-            const uint4 r4 = *reinterpret_cast<const uint4*>(red + (w2 * 4 + (lane >> 2)) * 16 + (lane & 3) * 4);
-            tj += (uint64_t)r4.x + r4.y + r4.z + r4.w;
+    {
+        int g = -1, o4 = 0;
+        if (lane >= 1 && lane <= 4) {
+            g = 0;
+            o4 = lane - 1;
+        } else if (NG > 0 && lane >= 16 && lane < 16 + 4 * NG) {
+            g = 1 + ((lane - 16) >> 2);
+            o4 = (lane - 16) & 3;
         }
-    } else if (lane == 16) {
+        if (g >= 0) {
 #pragma unroll 1
-        for (int w2 = 0; w2 < nw; ++w2) tj += red0[w2];
+            for (int w2 = 0; w2 < nw; ++w2) {
+                const uint4 r4 = *reinterpret_cast<const uint4*>(red + (w2 * 4 + g) * 16 + o4 * 4);
+                tj += (uint64_t)r4.x + r4.y + r4.z + r4.w;
+            }
+        } else if (lane == 0) {
+#pragma unroll 1
+            for (int w2 = 0; w2 < nw; ++w2) tj += red0[w2];
+        }
     }
-    const uint32_t tlo = (uint32_t)tj, thi = (uint32_t)(tj >> 32);
-    auto tot_at = [&](int j) __attribute__((always_inline)) -> uint64_t {
-        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)thi, j) << 32) |
-               (uint32_t)__builtin_amdgcn_readlane((int)tlo, j);
+    const bool cand = lane <= 4 || (lane >= 16 && lane < 16 + L);
+    uint64_t key = cand ? (tj << 4) | (uint64_t)(lane & 15) : ~0ull;
+    key = dpp_min_u64<0xB1>(key);  /* quad_perm [1,0,3,2] */
+    key = dpp_min_u64<0x4E>(key);  /* quad_perm [2,3,0,1] */
+    key = dpp_min_u64<0x141>(key); /* row_half_mirror */
+    key = dpp_min_u64<0x140>(key); /* row_mirror */
+    auto key_at = [&](int j) __attribute__((always_inline)) -> uint64_t {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), j) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, j);
     };
-    int fo = 0;
-    uint64_t fsum = tot_at(16);
-#pragma unroll
-    for (int o = 1; o < 5; ++o) {
-        const uint64_t v = tot_at(o - 1);
-        if (v < fsum) {
-            fsum = v;
-            fo = o;
-        }
-    }
+    const uint64_t fkey = key_at(0);
+    const int fo = (int)(fkey & 15);
+    const uint64_t fsum = fkey >> 4;
     int lbest = 0;
     uint64_t lsum = 0;
     bool lpc_wins = false, tie = false;
     if constexpr (NG > 0) {
-        lbest = 1;
-        lsum = tot_at(4);
-#pragma unroll
-        for (int pp = 2; pp <= 4 * NG; ++pp) {
-            if (pp <= L) {
-                const uint64_t v = tot_at(3 + pp);
-                if (v < lsum) {
-                    lsum = v;
-                    lbest = pp;
-                }
-            }
-        }
+        const uint64_t lkey = key_at(16);
+        lbest = (int)(lkey & 15) + 1;
+        lsum = lkey >> 4;
         /* a coefficient-less candidate sums |x| over all n (= the fixed order-0 sum), so it
          * never wins strictly */
         lpc_wins = lsum < fsum;
         tie = !lpc_wins && !(fsum < lsum);
     }
-    if (wid == 0 && a.fixed_sums) {
-        const uint64_t fv = (uint64_t)__shfl((unsigned long long)tj, lane == 0 ? 16 : (lane - 1) & 63);
-        if (lane < 5) a.fixed_sums[gid * 5 + lane] = (long long)fv;
-    }
+    if (wid == 0 && a.fixed_sums && lane < 5) a.fixed_sums[gid * 5 + lane] = (long long)tj;
     if (wid == 0 && a.lpc_sums) {
-        const uint64_t v = (uint64_t)__shfl((unsigned long long)tj, (lane + 4) & 63);
+        const uint64_t v = (uint64_t)__shfl((unsigned long long)tj, (lane + 16) & 63);
         if (lane < 32) a.lpc_sums[gid * 32 + lane] = (lane + 1 <= L) ? (long long)v : 0;
     }
     mv.fixed_order = fo;
