@@ -11,7 +11,7 @@
  * 386-404 with prediction_residual 537-548, the fixed-vs-LPC choice 133-157, encode_residual
  * + rice_partitions + find_rice_parameter + rice_size 632-760.
  *
- * Structure (nw = n/1536 rounded-up waves per workgroup, four workgroup barriers):
+ * Structure (nw = n/2560 rounded-up waves per workgroup, four workgroup barriers):
  *   - samples sit in LDS biased (x ^ 0x8000: unsigned 16-bit), which makes the MFMA operand
  *     build two byte permutes and two packed subtracts per lane and block;
  *   - candidate sums on v_mfma_f32_16x16x32_f16 with INTEGER taps and the accumulator
@@ -44,6 +44,16 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
+#ifndef FLACMI_STREAM_CPT
+#define FLACMI_STREAM_CPT 5
+#endif
+constexpr int kSCPT = FLACMI_STREAM_CPT; /* max 8-sample chunks per thread */
+/* workgroup size: 8-sample chunks, up to kSCPT per thread */
+__host__ __device__ inline int stream_threads(int n) {
+    const int nch = n / 8;
+    const int nt = 64 * ((nch + 64 * kSCPT - 1) / (64 * kSCPT));
+    return nt < 64 ? 64 : nt;
+}
 constexpr int kSHP = 16;                     /* biased-zero history pad in front of the unit (samples) */
 constexpr uint32_t kMagicBits = 0x4B400000u; /* 1.5 * 2^23 */
 constexpr int kCoefLimit = 127;              /* (sum|c| + 2^shift) * 33023 < 2^22 */
@@ -241,23 +251,23 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
     /* ---- stage: biased samples and the record into LDS, sum|x| on the way ---- */
     {
         const uint4* src = reinterpret_cast<const uint4*>((const int16_t*)a.samples + (a.unit0 + gid) * a.stride);
-        uint4 q[kCPT];
+        /* every load is issued before the first wait: clamped indices, no branches (a load
+         * inside a guarded block gets its own s_waitcnt there, serialising the HBM trips) */
+        uint4 q[kSCPT];
 #pragma unroll
-        for (int j = 0; j < kCPT; ++j)
-            if (tid + j * NT < nch) q[j] = src[tid + j * NT];
+        for (int j = 0; j < kSCPT; ++j) q[j] = src[min(tid + j * NT, nch - 1)];
         int32_t rv[2] = {0, 0};
         if constexpr (NG > 0) {
             const int32_t* r = a.rec + gid * a.rec_words;
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-                if (tid + j * NT < rw) rv[j] = r[tid + j * NT];
+            for (int j = 0; j < 2; ++j) rv[j] = r[min(tid + j * NT, rw - 1)];
         }
         if (tid < kSHP) xs[tid - kSHP] = 0x8000u; /* biased zeros */
         if (tid < Pmax) pks[tid] = 0;
         const uint32_t k8000 = opaque(0x8000u);
         uint32_t sumx = 0;
 #pragma unroll
-        for (int j = 0; j < kCPT; ++j) {
+        for (int j = 0; j < kSCPT; ++j) {
             const int v = tid + j * NT;
             if (v < nch) {
                 const uint4 y{q[j].x ^ 0x80008000u, q[j].y ^ 0x80008000u, q[j].z ^ 0x80008000u, q[j].w ^ 0x80008000u};
@@ -531,10 +541,10 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
                 break;
         }
     };
-    uint32_t zp[kCPT][4]; /* 16-bit pairs of the chunk's residual */
+    uint32_t zp[kSCPT][4]; /* 16-bit pairs of the chunk's residual */
     uint32_t big = 0;     /* bit j: chunk j holds a value >= 2^16 */
 #pragma unroll
-    for (int j = 0; j < kCPT; ++j) {
+    for (int j = 0; j < kSCPT; ++j) {
         const int c = tid + j * NT;
         zp[j][0] = zp[j][1] = zp[j][2] = zp[j][3] = 0;
         if (c < nch) {
@@ -610,7 +620,7 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
 #pragma unroll
     for (int o2 = 0; o2 < kRiceOrders; ++o2) tb[o2] = 0;
 #pragma unroll
-    for (int jc = 0; jc < kCPT; ++jc) {
+    for (int jc = 0; jc < kSCPT; ++jc) {
         const int c = tid + jc * NT;
         if (c < nch) {
             const int k = (int)(((float)c + 0.5f) * inv_cpp);
@@ -696,19 +706,19 @@ bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes) {
         return false;
     const bool ref = a.mode == FLACMI_MODE_REFERENCE && a.L >= 1 && a.L <= 12;
     if (!ref && a.mode != FLACMI_MODE_FIXED_ONLY) return false;
-    if (a.n % 64 != 0 || a.n < 64 || a.n > 8 * kCPT * 256) return false;
+    if (a.n % 64 != 0 || a.n < 64 || a.n > 8 * kSCPT * 256) return false;
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
     if (rmax_eff < 0 || (1 << rmax_eff) > 32 || ((a.n >> rmax_eff) & 7) != 0) return false; /* heap nodes < 64 */
-    const int nt = resid_threads(a.n);
+    const int nt = stream_threads(a.n);
     if (ref && a.rec_words > 2 * nt) return false;
     return true;
 }
 
 template <int NG>
 static hipError_t launch_stream_T(const ResidArgs& a, hipStream_t s) {
-    const int nt = resid_threads(a.n);
+    const int nt = stream_threads(a.n);
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
