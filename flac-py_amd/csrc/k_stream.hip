@@ -60,32 +60,81 @@ constexpr int kCoefLimit = 127;              /* (sum|c| + 2^shift) * 33023 < 2^2
 constexpr int kRiceOrders = 8;               /* orders 0..7 kept per finest partition */
 
 struct SLds {
-    int xs, rec, red, red0, red2, pks, pk, tap, bnd, mst, total;
+    int xs, pk, rec, red, red0, pks, tap, red2, mst, total;
 };
 
-/* MFMA tap table: 16 predictor columns (4 groups x 4 orders) x kTapN entries idx in
- * [-2, 16); entry idx holds the f16 pair (T[idx], T[idx-1]) where T[0] is the x[i] tap and
- * T[m+1] the coefficient of x[i-1-m] (0 outside the predictor), once plain (L: low sample
- * bytes) and once times 256 (H: high bytes). */
+/* MFMA tap table of the LPC groups: 4*NG predictor columns x kTapN entries idx in [-2, 16);
+ * entry idx holds the f16 pair (T[idx], T[idx-1]) where T[0] = -2^shift is the x[i] tap and
+ * T[m+1] the coefficient of x[i-1-m] (0 outside the predictor).  The high-byte operand is
+ * the same pair times 256 (one v_pk_mul_f16 per lane); the fixed group's operand is a
+ * constant (kFixB). */
 constexpr int kTapN = 18;
 
-__host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P) {
+/* Workgroup LDS (bytes).  Regions whose lifetimes do not overlap share space, which keeps a
+ * config-2 unit (n = 4608, two waves) at 11 KB: 14 workgroups per CU.
+ *   xs   biased samples behind a 16-sample zero pad             staging .. Rice recompute
+ *   pk   u16 [P][order] Rice parameters                         Rice (after B3)
+ *   rec  the unit's LPC record (aliases pk)                     staging .. choice (before B3)
+ *   red  u32 [nw][group][order][kb pair] MFMA partial sums      MFMA phase .. choice
+ *   red0 u32 [nw] sum|x|                                         staging .. choice
+ *   pks  u32 [P] finest partition sums                          staging (zeroed) .. Rice
+ *   tap  u32 [4*NG][kTapN] LPC taps                             after B1 .. MFMA prologue
+ *   red2 u64 [nw + 1][order] data bits (aliases tap)            Rice
+ *   mst  wave 0's 20 meta scalars (aliases tap, after red2)     exits after B1, final store */
+__host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P, int ng) {
     auto up = [](int b) { return (b + 15) & ~15; };
+    auto mx = [](int x, int y) { return x > y ? x : y; };
     SLds l;
     int o = 0;
     l.xs = o;   o = up(o + 2 * (kSHP + n));
-    l.rec = o;  o = up(o + 4 * (rec_words > 0 ? rec_words : 1));
-    l.red = o;  o = up(o + 4 * nw * 64);            /* u32 [nw][group][order][kb] */
-    l.red0 = o; o = up(o + 4 * nw);                 /* u32 [nw] sum|x| */
-    l.red2 = o; o = up(o + 8 * (nw + 1) * kRiceOrders); /* u64 [nw][order] data bits, [order] headers */
-    l.pks = o;  o = up(o + 4 * P);                  /* u32 finest partition sums */
-    l.pk = o;   o = up(o + P * 4 * kRiceOrders);    /* u32 [P][order] = p | p << 16 (every wave writes the same) */
-    l.tap = o;  o = up(o + 2 * 16 * kTapN * 4);     /* u32 [H|L][16 columns][kTapN] f16 pairs */
-    l.bnd = o;  o = up(o + 4 * 16);                 /* per LPC order: outside the MFMA exactness bound */
-    l.mst = o;  o = up(o + 4 * 20);                 /* wave 0: meta scalar fields */
+    l.pk = l.rec = o; o = up(o + mx(2 * P * kRiceOrders, 4 * mx(rec_words, 1)));
+    l.red = o;  o = up(o + 4 * nw * 32);
+    l.red0 = o; o = up(o + 4 * nw);
+    l.pks = o;  o = up(o + 4 * P);
+    const int r2 = 8 * (nw + 1) * kRiceOrders;
+    l.tap = l.red2 = o;
+    l.mst = o + r2;
+    o = up(o + mx(4 * 4 * ng * kTapN, r2 + 4 * 20));
     l.total = o;
     return l;
 }
+
+/* f16 bit pattern of a small integer (exact) */
+constexpr uint32_t f16_bits(int v) {
+    if (v == 0) return 0;
+    const uint32_t sgn = v < 0 ? 0x8000u : 0u;
+    const int m = v < 0 ? -v : v;
+    int e = 0;
+    while ((m >> (e + 1)) != 0) ++e;
+    return sgn | (uint32_t)((e + 15) << 10) | (uint32_t)((m << (10 - e)) & 0x3ff);
+}
+/* fixed predictor order p (common.py:15-21) as taps: T[0] = -1 (x[i]), T[j] = (-1)^(j-1) C(p, j) */
+constexpr int fixed_tap(int p, int j) {
+    if (j == 0) return -1;
+    if (j < 0 || j > p) return 0;
+    int c = 1;
+    for (int t = 0; t < j; ++t) c = c * (p - t) / (t + 1);
+    return (j & 1) ? c : -c;
+}
+/* the fixed group's B operand per lane (column = 4 (order - 1) + phase rho, kb = lane / 16):
+ * {H(ia), H(ia - 2), L(ia), L(ia - 2)}, ia = 12 + rho - 4 kb, L(i) = (T[i], T[i-1]), H = 256 L */
+struct FixB {
+    uint32_t w[64 * 4];
+};
+constexpr FixB make_fixb() {
+    FixB t{};
+    for (int l = 0; l < 64; ++l) {
+        const int col = l & 15, kb = l >> 4, p = (col >> 2) + 1, rho = col & 3, ia = 12 + rho - 4 * kb;
+        const int idx[2] = {ia, ia - 2};
+        for (int k = 0; k < 2; ++k) {
+            const int i = idx[k];
+            t.w[4 * l + k] = f16_bits(256 * fixed_tap(p, i)) | f16_bits(256 * fixed_tap(p, i - 1)) << 16;
+            t.w[4 * l + 2 + k] = f16_bits(fixed_tap(p, i)) | f16_bits(fixed_tap(p, i - 1)) << 16;
+        }
+    }
+    return t;
+}
+__constant__ const FixB kFixB = make_fixb();
 
 /* |a - b| + acc: the compiler emits one v_sad_u32 when b is in a VGPR (opaque() keeps a
  * constant b there).  Not inline asm: the hazard recognizer does not see an asm operand
@@ -222,7 +271,7 @@ __device__ __forceinline__ void store_meta(flacmi_unit_meta* m, int lane, const 
 /* NG = number of LPC MFMA groups (ceil(L / 4)), 0 in fixed-only mode.  One workgroup per
  * unit; every exit is workgroup-uniform (all waves decide from the same LDS data). */
 template <int NG>
-__global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_resid_stream(ResidArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, nw = NT >> 6;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -234,21 +283,21 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (n % (1 << o) == 0) rmax_eff = o;
     const int Pmax = 1 << rmax_eff; /* host-checked: 0 <= rmax_eff <= 5 */
-    const SLds lay = stream_lds(n, nw, rw, Pmax);
+    const SLds lay = stream_lds(n, nw, rw, Pmax, NG);
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem + lay.xs) + kSHP;
     int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.rec);
     uint32_t* red = reinterpret_cast<uint32_t*>(smem + lay.red);
     uint32_t* red0 = reinterpret_cast<uint32_t*>(smem + lay.red0);
     unsigned long long* red2 = reinterpret_cast<unsigned long long*>(smem + lay.red2);
     uint32_t* pks = reinterpret_cast<uint32_t*>(smem + lay.pks); /* finest partition sums */
-    uint32_t* pkw = reinterpret_cast<uint32_t*>(smem + lay.pk);
+    uint16_t* pkw = reinterpret_cast<uint16_t*>(smem + lay.pk);
     uint32_t* tap = reinterpret_cast<uint32_t*>(smem + lay.tap);
-    int* bnd = reinterpret_cast<int*>(smem + lay.bnd);
     uint32_t* mst = reinterpret_cast<uint32_t*>(smem + lay.mst);
     flacmi_unit_meta* meta = a.meta + gid;
     MetaVals mv{};
 
     /* ---- stage: biased samples and the record into LDS, sum|x| on the way ---- */
+    uint4 fixb; /* the fixed group's MFMA B operand (constant) */
     {
         const uint4* src = reinterpret_cast<const uint4*>((const int16_t*)a.samples + (a.unit0 + gid) * a.stride);
         /* every load is issued before the first wait: clamped indices, no branches (a load
@@ -256,6 +305,7 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         uint4 q[kSCPT];
 #pragma unroll
         for (int j = 0; j < kSCPT; ++j) q[j] = src[min(tid + j * NT, nch - 1)];
+        fixb = reinterpret_cast<const uint4*>(kFixB.w)[lane];
         int32_t rv[2] = {0, 0};
         if constexpr (NG > 0) {
             const int32_t* r = a.rec + gid * a.rec_words;
@@ -289,57 +339,8 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         if (lane == 0) red0[wid] = sx;
     }
     __syncthreads(); /* B1 */
-    /* the MFMA tap table (and, per LPC order, the exactness bound) from the staged record */
-    {
-        const int32_t* rg = recl;
-        for (int e = tid; e < 4 * (NG + 1) * kTapN; e += NT) {
-            const int col = e / kTapN, idx = e - col * kTapN - 2, g = col >> 2, o4 = col & 3;
-            int p = o4 + 1, sh = 0;
-            const int32_t* cp = rg;
-            bool live = true;
-            if (g > 0) {
-                p = 4 * (g - 1) + o4 + 1;
-                live = NG > 0 && p <= L;
-                if (live) {
-                    sh = rg[2 + p - 1];
-                    cp = rg + 2 + L + (p * (p - 1)) / 2;
-                }
-            }
-            float t2[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int ix = idx - h;
-                float v = 0.0f;
-                if (live && ix == 0) {
-                    v = g == 0 ? -1.0f : -(float)(1 << sh);
-                } else if (live && ix >= 1 && ix <= p) {
-                    const int m = ix - 1;
-                    if (g == 0) { /* fixed order p (common.py:15-21): x[i-1-m] weighs (-1)^m C(p, m+1) */
-                        const int c1 = p, c2 = p * (p - 1) / 2, c3 = p * (p - 1) * (p - 2) / 6,
-                                  c4 = p * (p - 1) * (p - 2) * (p - 3) / 24;
-                        v = (float)(m == 0 ? c1 : m == 1 ? -c2 : m == 2 ? c3 : -c4);
-                    } else {
-                        v = (float)cp[m];
-                    }
-                }
-                t2[h] = v;
-            }
-            tap[col * kTapN + idx + 2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t2[0], 256.0f * t2[1]));
-            tap[(16 + col) * kTapN + idx + 2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t2[0], t2[1]));
-            if (NG > 0 && g > 0 && idx == 0 && live) { /* (sum|c| + 2^shift) * 33023 < 2^22 */
-                int c[4 * (NG > 0 ? NG : 1)];
-#pragma unroll
-                for (int m = 0; m < 4 * (NG > 0 ? NG : 1); ++m) c[m] = m < p ? cp[m] : 0; /* independent reads */
-                int sa = 1 << sh;
-#pragma unroll
-                for (int m = 0; m < 4 * (NG > 0 ? NG : 1); ++m) sa += c[m] < 0 ? -c[m] : c[m];
-                bnd[p - 1] = sa > kCoefLimit;
-            }
-        }
-    }
-    __syncthreads(); /* B1b: tap table */
-
-    /* ---- unit status from the LPC record; MFMA exactness bound per order ---- */
+    /* ---- unit status from the LPC record; MFMA exactness bound per order; LPC tap table.
+     * Every wave reads the same LDS words, so the exits are workgroup-uniform. ---- */
     uint32_t negmask = 0;
     if constexpr (NG > 0) {
         const int st = recl[0];
@@ -352,7 +353,18 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
             return;
         }
         negmask = (uint32_t)recl[1];
-        if (__ballot(lane < L && bnd[lane < L ? lane : 0])) { /* outside the exactness bound: k_resid redoes it */
+        int sa = 0; /* lane p - 1: (sum|c| + 2^shift) of order p; * 33023 < 2^22 keeps the MFMA exact */
+        if (lane < L) {
+            const int p = lane + 1, sh = recl[2 + lane];
+            const int32_t* cp = recl + 2 + L + (p * (p - 1)) / 2;
+            int c[4 * NG];
+#pragma unroll
+            for (int m = 0; m < 4 * NG; ++m) c[m] = m < p ? cp[m] : 0; /* independent reads */
+            sa = 1 << sh;
+#pragma unroll
+            for (int m = 0; m < 4 * NG; ++m) sa += c[m] < 0 ? -c[m] : c[m];
+        }
+        if (__ballot(sa > kCoefLimit)) { /* outside the exactness bound: k_resid redoes it */
             if (tid == 0) {
                 meta->status = FLACMI_STATUS_RETRY;
                 const unsigned long long k = atomicAdd(a.retry_count, 1ull);
@@ -360,7 +372,24 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
             }
             return;
         }
+        for (int e = tid; e < 4 * NG * kTapN; e += NT) {
+            const int col = e / kTapN, idx = e - col * kTapN - 2, p = col + 1;
+            const bool live = p <= L;
+            const int sh = live ? recl[2 + p - 1] : 0;
+            const int32_t* cp = recl + 2 + L + (p * (p - 1)) / 2;
+            float t2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int ix = idx - h;
+                int v = 0;
+                if (ix == 0) v = -(1 << sh);
+                else if (ix >= 1 && ix <= p) v = cp[ix - 1];
+                t2[h] = live ? (float)v : 0.0f;
+            }
+            tap[e] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t2[0], t2[1]));
+        }
     }
+    __syncthreads(); /* B1b: tap table */
     if (a.stop_after == 1) return;
 
     /* ---- candidate sums on MFMA ---- */
@@ -372,9 +401,15 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         const int idx0 = 12 + rho - 4 * kb + 2; /* table position of tap jj = 0 */
 #pragma unroll
         for (int g = 0; g <= NG; ++g) {
-            const uint32_t* th = tap + (4 * g + o4) * kTapN;
-            const uint32_t* tl = tap + (16 + 4 * g + o4) * kTapN;
-            B[g] = __builtin_bit_cast(h8, uint4{th[idx0], th[idx0 - 2], tl[idx0], tl[idx0 - 2]});
+            if (g == 0) {
+                B[0] = __builtin_bit_cast(h8, fixb);
+            } else {
+                const uint32_t* tl = tap + (4 * (g - 1) + o4) * kTapN;
+                const uint32_t l0 = tl[idx0], l2 = tl[idx0 - 2];
+                const uint32_t h0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, l0) * h2{256, 256});
+                const uint32_t hh = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, l2) * h2{256, 256});
+                B[g] = __builtin_bit_cast(h8, uint4{h0, hh, l0, l2});
+            }
             int sh = 0, start = o4 + 1;
             if (g > 0) {
                 const int p = 4 * (g - 1) + o4 + 1;
@@ -432,7 +467,8 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
             uint32_t v = acc[g];
             v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
             v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
-            if (rho == 0) red[(wid * 4 + g) * 16 + o4 * 4 + kb] = v;
+            v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F); /* lane ^ 16: kb pairs */
+            if (rho == 0 && (kb & 1) == 0) red[(wid * 4 + g) * 8 + o4 * 2 + (kb >> 1)] = v;
         }
     }
     __syncthreads(); /* B2 */
@@ -455,8 +491,8 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         if (g >= 0) {
 #pragma unroll 1
             for (int w2 = 0; w2 < nw; ++w2) {
-                const uint4 r4 = *reinterpret_cast<const uint4*>(red + (w2 * 4 + g) * 16 + o4 * 4);
-                tj += (uint64_t)r4.x + r4.y + r4.z + r4.w;
+                const uint2 r2 = *reinterpret_cast<const uint2*>(red + (w2 * 4 + g) * 8 + o4 * 2);
+                tj += (uint64_t)r2.x + r2.y;
             }
         } else if (lane == 0) {
 #pragma unroll 1
@@ -611,7 +647,7 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         if (o2 >= ro && o2 <= oo) {
             const int node = (1 << o2) + (lane >> (oo - o2));
             const int pv = __shfl(prm, (node - 1) & 63);
-            if (lane < P) pkw[lane * kRiceOrders + o2] = (uint32_t)pv * 0x10001u;
+            if (lane < P) pkw[lane * kRiceOrders + o2] = (uint16_t)pv;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -624,9 +660,12 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
         const int c = tid + jc * NT;
         if (c < nch) {
             const int k = (int)(((float)c + 0.5f) * inv_cpp);
-            const uint4 p0 = *reinterpret_cast<const uint4*>(pkw + k * kRiceOrders);
-            const uint4 p1 = *reinterpret_cast<const uint4*>(pkw + k * kRiceOrders + 4);
-            const uint32_t pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+            const uint4 pq = *reinterpret_cast<const uint4*>(pkw + k * kRiceOrders);
+            const uint32_t pw[4] = {pq.x, pq.y, pq.z, pq.w};
+            uint32_t pv[8]; /* p | p << 16 per order */
+#pragma unroll
+            for (int o2 = 0; o2 < kRiceOrders; ++o2)
+                pv[o2] = __builtin_amdgcn_perm(pw[o2 >> 1], pw[o2 >> 1], (o2 & 1) ? 0x03020302u : 0x01000100u);
             if (!((big >> jc) & 1)) {
 #pragma unroll
                 for (int o2 = 0; o2 < kRiceOrders; ++o2)
@@ -693,7 +732,7 @@ __global__ __launch_bounds__(256) void k_resid_stream(ResidArgs a) {
     mv.rice_bits = (long long)bb;
     store_meta(meta, lane, mv, coefl, mst);
     int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
-    if (lane < (1 << best)) rp[lane] = (int32_t)(pkw[(lane << (oo - best)) * kRiceOrders + best] & 0xffffu);
+    if (lane < (1 << best)) rp[lane] = (int32_t)pkw[(lane << (oo - best)) * kRiceOrders + best];
 }
 
 /* units the stream kernel listed (outside its MFMA bound) are handled by k_resid's list
@@ -722,7 +761,7 @@ static hipError_t launch_stream_T(const ResidArgs& a, hipStream_t s) {
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
-    const size_t lds = stream_lds(a.n, nt / 64, NG > 0 ? a.rec_words : 0, 1 << rmax_eff).total;
+    const size_t lds = stream_lds(a.n, nt / 64, NG > 0 ? a.rec_words : 0, 1 << rmax_eff, NG).total;
     auto kern = k_resid_stream<NG>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
