@@ -22,8 +22,8 @@
  *     (bits >> shift) - (0x4B400000 >> shift) = floor(T / 2^shift) = -r exactly.  Fixed
  *     predictors (shift 0): |r| is one v_sad_u32; LPC: one shift + one v_sad_u32.
  *     MFMA 0 holds fixed orders 1..4 x 4 sample phases, MFMAs 1..NG the LPC orders
- *     4(g-1)+1 .. 4g x 4 phases, from a tap table built once per unit in LDS.  Units
- *     outside the bound are listed for k_resid;
+ *     4(g-1)+1 .. 4g x 4 phases; each lane builds its B operands from the LDS record (the
+ *     fixed group's is a constant).  Units outside the bound are listed for k_resid;
  *   - the choice (a lane-parallel DPP argmin), the Rice parameters (one heap node per lane,
  *     finest partition sums by LDS atomics) and the order choice are
  *     computed redundantly by every wave from LDS data, so no single-wave serial section
@@ -33,6 +33,8 @@
  *     values are < 2^16;
  *   - the 208-byte meta record is one coalesced store of 52 lanes.
  */
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace flacmi {
@@ -60,41 +62,28 @@ constexpr int kCoefLimit = 127;              /* (sum|c| + 2^shift) * 33023 < 2^2
 constexpr int kRiceOrders = 8;               /* orders 0..7 kept per finest partition */
 
 struct SLds {
-    int xs, pk, rec, red, red0, pks, tap, red2, mst, total;
+    int xs, pk, rec, red, red2, red0, pks, total;
 };
 
-/* MFMA tap table of the LPC groups: 4*NG predictor columns x kTapN entries idx in [-2, 16);
- * entry idx holds the f16 pair (T[idx], T[idx-1]) where T[0] = -2^shift is the x[i] tap and
- * T[m+1] the coefficient of x[i-1-m] (0 outside the predictor).  The high-byte operand is
- * the same pair times 256 (one v_pk_mul_f16 per lane); the fixed group's operand is a
- * constant (kFixB). */
-constexpr int kTapN = 18;
-
 /* Workgroup LDS (bytes).  Regions whose lifetimes do not overlap share space, which keeps a
- * config-2 unit (n = 4608, two waves) at 11 KB: 14 workgroups per CU.
+ * config-2 unit (n = 4608, two waves) at 10160 B: 16 workgroups per CU.
  *   xs   biased samples behind a 16-sample zero pad             staging .. Rice recompute
  *   pk   u16 [P][order] Rice parameters                         Rice (after B3)
  *   rec  the unit's LPC record (aliases pk)                     staging .. choice (before B3)
  *   red  u32 [nw][group][order][kb pair] MFMA partial sums      MFMA phase .. choice
+ *   red2 u64 [nw + 1][order] data bits (aliases red)            Rice (after B3)
  *   red0 u32 [nw] sum|x|                                         staging .. choice
- *   pks  u32 [P] finest partition sums                          staging (zeroed) .. Rice
- *   tap  u32 [4*NG][kTapN] LPC taps                             after B1 .. MFMA prologue
- *   red2 u64 [nw + 1][order] data bits (aliases tap)            Rice
- *   mst  wave 0's 20 meta scalars (aliases tap, after red2)     exits after B1, final store */
-__host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P, int ng) {
+ *   pks  u32 [P] finest partition sums                          staging (zeroed) .. Rice */
+__host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P) {
     auto up = [](int b) { return (b + 15) & ~15; };
     auto mx = [](int x, int y) { return x > y ? x : y; };
     SLds l;
     int o = 0;
     l.xs = o;   o = up(o + 2 * (kSHP + n));
     l.pk = l.rec = o; o = up(o + mx(2 * P * kRiceOrders, 4 * mx(rec_words, 1)));
-    l.red = o;  o = up(o + 4 * nw * 32);
+    l.red = l.red2 = o; o = up(o + mx(4 * nw * 32, 8 * (nw + 1) * kRiceOrders));
     l.red0 = o; o = up(o + 4 * nw);
     l.pks = o;  o = up(o + 4 * P);
-    const int r2 = 8 * (nw + 1) * kRiceOrders;
-    l.tap = l.red2 = o;
-    l.mst = o + r2;
-    o = up(o + mx(4 * 4 * ng * kTapN, r2 + 4 * 20));
     l.total = o;
     return l;
 }
@@ -242,36 +231,36 @@ __device__ __forceinline__ void lpc_chunk(const uint16_t* xs, int i0, int32_t co
 }
 
 /* One wave writes the 52 dwords of a unit's flacmi_unit_meta (include/flacmi.h field order)
- * with one store: lane 0 stages the 20 scalar fields in LDS (mst), lanes 20..51 take
+ * with one store: lanes 0..19 take the 20 scalar fields (a select chain), lanes 20..51 take
  * coefs[lane - 20] from lane q's `coef`. */
 struct MetaVals {
     int status, site, kind, order, shift, ncoefs, res_offset, res_len, fixed_order, lpc_order, part_order,
         n_parts, coding;
     long long fixed_sum, lpc_sum, rice_bits;
 };
-__device__ __forceinline__ void store_meta(flacmi_unit_meta* m, int lane, const MetaVals& v, int32_t coef,
-                                           uint32_t* mst) {
-    if (lane == 0) {
-        uint4* d = reinterpret_cast<uint4*>(mst);
-        d[0] = uint4{(uint32_t)v.status, (uint32_t)v.site, (uint32_t)v.kind, (uint32_t)v.order};
-        d[1] = uint4{(uint32_t)v.shift, (uint32_t)v.ncoefs, (uint32_t)v.res_offset, (uint32_t)v.res_len};
-        d[2] = uint4{(uint32_t)v.fixed_order, (uint32_t)v.lpc_order, (uint32_t)v.part_order, (uint32_t)v.n_parts};
-        d[3] = uint4{(uint32_t)v.coding, 0u, (uint32_t)v.fixed_sum, (uint32_t)((unsigned long long)v.fixed_sum >> 32)};
-        d[4] = uint4{(uint32_t)v.lpc_sum, (uint32_t)((unsigned long long)v.lpc_sum >> 32), (uint32_t)v.rice_bits,
-                     (uint32_t)((unsigned long long)v.rice_bits >> 32)};
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t cq = (uint32_t)__shfl(coef, (lane - 20) & 63);
-    const uint32_t x = lane < 20 ? mst[lane < 20 ? lane : 0] : cq;
+__device__ __forceinline__ void store_meta(flacmi_unit_meta* m, int lane, const MetaVals& v, int32_t coef) {
+    uint32_t x = (uint32_t)__shfl(coef, (lane - 20) & 63);
+    const uint32_t f[20] = {(uint32_t)v.status, (uint32_t)v.site, (uint32_t)v.kind, (uint32_t)v.order,
+                            (uint32_t)v.shift, (uint32_t)v.ncoefs, (uint32_t)v.res_offset, (uint32_t)v.res_len,
+                            (uint32_t)v.fixed_order, (uint32_t)v.lpc_order, (uint32_t)v.part_order,
+                            (uint32_t)v.n_parts, (uint32_t)v.coding, 0u, (uint32_t)v.fixed_sum,
+                            (uint32_t)((unsigned long long)v.fixed_sum >> 32), (uint32_t)v.lpc_sum,
+                            (uint32_t)((unsigned long long)v.lpc_sum >> 32), (uint32_t)v.rice_bits,
+                            (uint32_t)((unsigned long long)v.rice_bits >> 32)};
+#pragma unroll
+    for (int i = 0; i < 20; ++i) x = lane == i ? f[i] : x;
     if (lane < 52) reinterpret_cast<uint32_t*>(m)[lane] = x;
 }
 
 }  // namespace
 
-/* NG = number of LPC MFMA groups (ceil(L / 4)), 0 in fixed-only mode.  One workgroup per
- * unit; every exit is workgroup-uniform (all waves decide from the same LDS data). */
-template <int NG>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_resid_stream(ResidArgs a) {
+/* NG = number of LPC MFMA groups (ceil(L / 4)), 0 in fixed-only mode.  R05: the Rice
+ * partition orders are 0..5 for every unit (host-checked: rmin 0, n % 32 == 0 and n / 32 >
+ * every predictor order), so the order loops compile without per-order branches.  One
+ * workgroup per unit; every exit is workgroup-uniform (all waves decide from the same LDS
+ * data). */
+template <int NG, bool R05>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7, 8))) void k_resid_stream(ResidArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, nw = NT >> 6;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -283,7 +272,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (n % (1 << o) == 0) rmax_eff = o;
     const int Pmax = 1 << rmax_eff; /* host-checked: 0 <= rmax_eff <= 5 */
-    const SLds lay = stream_lds(n, nw, rw, Pmax, NG);
+    const SLds lay = stream_lds(n, nw, rw, Pmax);
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem + lay.xs) + kSHP;
     int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.rec);
     uint32_t* red = reinterpret_cast<uint32_t*>(smem + lay.red);
@@ -291,8 +280,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     unsigned long long* red2 = reinterpret_cast<unsigned long long*>(smem + lay.red2);
     uint32_t* pks = reinterpret_cast<uint32_t*>(smem + lay.pks); /* finest partition sums */
     uint16_t* pkw = reinterpret_cast<uint16_t*>(smem + lay.pk);
-    uint32_t* tap = reinterpret_cast<uint32_t*>(smem + lay.tap);
-    uint32_t* mst = reinterpret_cast<uint32_t*>(smem + lay.mst);
     flacmi_unit_meta* meta = a.meta + gid;
     MetaVals mv{};
 
@@ -339,7 +326,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
         if (lane == 0) red0[wid] = sx;
     }
     __syncthreads(); /* B1 */
-    /* ---- unit status from the LPC record; MFMA exactness bound per order; LPC tap table.
+    /* ---- unit status from the LPC record; MFMA exactness bound per order.
      * Every wave reads the same LDS words, so the exits are workgroup-uniform. ---- */
     uint32_t negmask = 0;
     if constexpr (NG > 0) {
@@ -348,7 +335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
             if (wid == 0) {
                 mv.status = st & 0xffff;
                 mv.site = st >> 16;
-                store_meta(meta, lane, mv, 0, mst);
+                store_meta(meta, lane, mv, 0);
             }
             return;
         }
@@ -372,24 +359,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
             }
             return;
         }
-        for (int e = tid; e < 4 * NG * kTapN; e += NT) {
-            const int col = e / kTapN, idx = e - col * kTapN - 2, p = col + 1;
-            const bool live = p <= L;
-            const int sh = live ? recl[2 + p - 1] : 0;
-            const int32_t* cp = recl + 2 + L + (p * (p - 1)) / 2;
-            float t2[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int ix = idx - h;
-                int v = 0;
-                if (ix == 0) v = -(1 << sh);
-                else if (ix >= 1 && ix <= p) v = cp[ix - 1];
-                t2[h] = live ? (float)v : 0.0f;
-            }
-            tap[e] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t2[0], t2[1]));
-        }
     }
-    __syncthreads(); /* B1b: tap table */
     if (a.stop_after == 1) return;
 
     /* ---- candidate sums on MFMA ---- */
@@ -398,16 +368,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
         h8 B[NG + 1];
         int shg[NG + 1], startg[NG + 1];
         uint32_t kg[NG + 1];
-        const int idx0 = 12 + rho - 4 * kb + 2; /* table position of tap jj = 0 */
+        const int idx0 = 12 + rho - 4 * kb + 2; /* tap index of the lane's first operand pair, + 2 */
 #pragma unroll
         for (int g = 0; g <= NG; ++g) {
             if (g == 0) {
                 B[0] = __builtin_bit_cast(h8, fixb);
-            } else {
-                const uint32_t* tl = tap + (4 * (g - 1) + o4) * kTapN;
-                const uint32_t l0 = tl[idx0], l2 = tl[idx0 - 2];
-                const uint32_t h0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, l0) * h2{256, 256});
-                const uint32_t hh = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, l2) * h2{256, 256});
+            } else { /* taps T[ia], T[ia-1], T[ia-2], T[ia-3] of LPC order p from the record */
+                const int p = 4 * (g - 1) + o4 + 1, ia = idx0 - 2;
+                const bool live = p <= L;
+                const int sh = live ? recl[2 + p - 1] : 0;
+                const int32_t* cp = recl + 2 + L + (p * (p - 1)) / 2;
+                float t[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int m = ia - u;
+                    int v = 0;
+                    if (m == 0) v = -(1 << sh);
+                    else if (m >= 1 && m <= p) v = cp[m - 1];
+                    t[u] = live ? (float)v : 0.0f;
+                }
+                const uint32_t l0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t[0], t[1]));
+                const uint32_t l2 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t[2], t[3]));
+                const uint32_t h0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[0], 256.0f * t[1]));
+                const uint32_t hh = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[2], 256.0f * t[3]));
                 B[g] = __builtin_bit_cast(h8, uint4{h0, hh, l0, l2});
             }
             int sh = 0, start = o4 + 1;
@@ -537,7 +520,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
         if (wid == 0) {
             mv.status = ST_ASSERT;
             mv.site = FLACMI_SITE_CHOICE_TIE;
-            store_meta(meta, lane, mv, 0, mst);
+            store_meta(meta, lane, mv, 0);
         }
         return;
     }
@@ -557,9 +540,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
      * pairs when every value of the chunk is < 2^16 (else recomputed for the Rice pass);
      * finest partition sums by LDS atomics ---- */
     const int order = mv.order;
-    int omax = -1;
-    for (int o = a.rmin; o <= a.rmax; ++o)
-        if ((n % (1 << o)) == 0 && (n >> o) > order) omax = o;
+    int omax = R05 ? 5 : -1;
+    if constexpr (!R05)
+        for (int o = a.rmin; o <= a.rmax; ++o)
+            if ((n % (1 << o)) == 0 && (n >> o) > order) omax = o;
     const int P = 1 << (omax < 0 ? 0 : omax), cpp = (n >> (omax < 0 ? 0 : omax)) >> 3;
     const float inv_cpp = 1.0f / (float)cpp;
     uint32_t* __restrict__ rout = reinterpret_cast<uint32_t*>(a.residual) + gid * a.residual_stride;
@@ -579,21 +563,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     };
     uint32_t zp[kSCPT][4]; /* 16-bit pairs of the chunk's residual */
     uint32_t big = 0;     /* bit j: chunk j holds a value >= 2^16 */
+    /* one copy of the chunk loop per predictor (the switch is taken once, not per chunk) */
+    auto residual_pass = [&](auto kk) __attribute__((always_inline)) {
+        constexpr int KK = decltype(kk)::value;
 #pragma unroll
-    for (int j = 0; j < kSCPT; ++j) {
-        const int c = tid + j * NT;
-        zp[j][0] = zp[j][1] = zp[j][2] = zp[j][3] = 0;
-        if (c < nch) {
-            uint32_t z[8];
-            resid(c, z);
-            reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{z[0], z[1], z[2], z[3]};
-            reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{z[4], z[5], z[6], z[7]};
-            const uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
-            if (omax >= 0) atomicAdd(&pks[(int)(((float)c + 0.5f) * inv_cpp)], cs);
-            if ((z[0] | z[1] | z[2] | z[3] | z[4] | z[5] | z[6] | z[7]) >> 16) big |= 1u << j;
+        for (int j = 0; j < kSCPT; ++j) {
+            const int c = tid + j * NT;
+            zp[j][0] = zp[j][1] = zp[j][2] = zp[j][3] = 0;
+            if (c < nch) {
+                uint32_t z[8];
+                if constexpr (KK >= 0) fixed_chunk<KK>(xs, 8 * c, z);
+                else lpc_chunk(xs, 8 * c, coefl, lsh, order, z);
+                reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{z[0], z[1], z[2], z[3]};
+                reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{z[4], z[5], z[6], z[7]};
+                const uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
+                if (omax >= 0) atomicAdd(&pks[(int)(((float)c + 0.5f) * inv_cpp)], cs);
+                if ((z[0] | z[1] | z[2] | z[3] | z[4] | z[5] | z[6] | z[7]) >> 16) big |= 1u << j;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) zp[j][i] = __builtin_amdgcn_perm(z[2 * i + 1], z[2 * i], 0x05040100u);
+                for (int i = 0; i < 4; ++i) zp[j][i] = __builtin_amdgcn_perm(z[2 * i + 1], z[2 * i], 0x05040100u);
+            }
         }
+    };
+    switch (fixed_k) {
+        case 0: residual_pass(std::integral_constant<int, 0>{}); break;
+        case 1: residual_pass(std::integral_constant<int, 1>{}); break;
+        case 2: residual_pass(std::integral_constant<int, 2>{}); break;
+        case 3: residual_pass(std::integral_constant<int, 3>{}); break;
+        case 4: residual_pass(std::integral_constant<int, 4>{}); break;
+        default:
+            if constexpr (NG > 0) residual_pass(std::integral_constant<int, -1>{});
+            break;
     }
     __syncthreads(); /* B3 */
     if (a.stop_after == 4) return;
@@ -603,11 +602,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
         if (wid == 0) {
             mv.status = ST_ASSERT;
             mv.site = FLACMI_SITE_RICE_NO_ORDER;
-            store_meta(meta, lane, mv, coefl, mst);
+            store_meta(meta, lane, mv, coefl);
         }
         return;
     }
-    const int ro = __builtin_amdgcn_readfirstlane(a.rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+    const int ro = R05 ? 0 : __builtin_amdgcn_readfirstlane(a.rmin), oo = R05 ? 5 : __builtin_amdgcn_readfirstlane(omax);
     /* every wave, lane j - 1 = heap node j = (order o, partition K), j = 2^o + K < 2P <= 64:
      * node sums from a prefix over the finest sums, one parameter each, the first error in
      * the reference's evaluation order = the lowest node (orders ascending, then partitions) */
@@ -635,7 +634,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
                 const int kl = __builtin_ctzll(eb);
                 mv.status = ST_VALUE;
                 mv.site = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
-                store_meta(meta, lane, mv, coefl, mst);
+                store_meta(meta, lane, mv, coefl);
             }
             return;
         }
@@ -730,7 +729,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8))) voi
     mv.n_parts = 1 << best;
     mv.coding = ((m5 >> best) & 1) ? 5 : 4;
     mv.rice_bits = (long long)bb;
-    store_meta(meta, lane, mv, coefl, mst);
+    store_meta(meta, lane, mv, coefl);
     int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
     if (lane < (1 << best)) rp[lane] = (int32_t)pkw[(lane << (oo - best)) * kRiceOrders + best];
 }
@@ -755,18 +754,30 @@ bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes) {
     return true;
 }
 
-template <int NG>
-static hipError_t launch_stream_T(const ResidArgs& a, hipStream_t s) {
+template <int NG, bool R05>
+static hipError_t launch_stream_R(const ResidArgs& a, hipStream_t s) {
     const int nt = stream_threads(a.n);
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
-    const size_t lds = stream_lds(a.n, nt / 64, NG > 0 ? a.rec_words : 0, 1 << rmax_eff, NG).total;
-    auto kern = k_resid_stream<NG>;
+    const size_t lds = stream_lds(a.n, nt / 64, NG > 0 ? a.rec_words : 0, 1 << rmax_eff).total;
+    auto kern = k_resid_stream<NG, R05>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)a.count), dim3(nt), lds, s, a);
     return hipGetLastError();
+}
+
+template <int NG>
+static hipError_t launch_stream_T(const ResidArgs& a, hipStream_t s) {
+    /* partition orders 0..5 for every unit: rmin 0, rmax_eff 5 and n / 32 above the largest
+     * predictor order (4 fixed, L for LPC) */
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (a.n % (1 << o) == 0) rmax_eff = o;
+    const int maxord = NG > 0 && a.L > 4 ? a.L : 4;
+    if (a.rmin == 0 && rmax_eff == 5 && (a.n >> 5) > maxord) return launch_stream_R<NG, true>(a, s);
+    return launch_stream_R<NG, false>(a, s);
 }
 
 hipError_t launch_resid_stream(const ResidArgs& a, hipStream_t s) {
