@@ -263,6 +263,14 @@ template <int NG, bool R05>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7, 8))) void k_resid_stream(ResidArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, nw = NT >> 6;
+#if FLACMI_STREAM_STAMPS /* diagnostic build only: per-unit phase clock stamps of wave 0 */
+    uint64_t stamp[8];
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    stamp[0] = __builtin_amdgcn_s_memtime();
+#define STAMP(k) (stamp[k] = __builtin_amdgcn_s_memtime())
+#else
+#define STAMP(k) ((void)0)
+#endif
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t gid = blockIdx.x;
     const int n = a.n, L = NG > 0 ? a.L : 0;
@@ -325,7 +333,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         const uint32_t sx = wave_sum_u32(sumx);
         if (lane == 0) red0[wid] = sx;
     }
+    STAMP(1);
     __syncthreads(); /* B1 */
+    STAMP(2);
     /* ---- unit status from the LPC record; MFMA exactness bound per order.
      * Every wave reads the same LDS words, so the exits are workgroup-uniform. ---- */
     uint32_t negmask = 0;
@@ -455,6 +465,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         }
     }
     __syncthreads(); /* B2 */
+    STAMP(3);
     if (a.stop_after == 2) return;
 
     /* ---- choice (encoder.py:331-359, 398-404, 135-157), every wave, lane-parallel ----
@@ -535,6 +546,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         }
     }
     if (a.stop_after == 3) return;
+    STAMP(4);
 
     /* ---- chosen residual: zig-zag (utils.py:91-94) to HBM; kept in registers as 16-bit
      * pairs when every value of the chunk is < 2^16 (else recomputed for the Rice pass);
@@ -595,6 +607,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             break;
     }
     __syncthreads(); /* B3 */
+    STAMP(5);
     if (a.stop_after == 4) return;
 
     /* ---- Rice partition search (encoder.py:655-760) ---- */
@@ -701,6 +714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             }
     }
     __syncthreads(); /* B4 */
+    STAMP(6);
     if (wid != 0) return;
     /* wave 0: headers per order (lanes of that order's nodes), totals, first minimum */
     const uint32_t hb = valid ? 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm) : 0u;
@@ -730,6 +744,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     mv.coding = ((m5 >> best) & 1) ? 5 : 4;
     mv.rice_bits = (long long)bb;
     store_meta(meta, lane, mv, coefl);
+#if FLACMI_STREAM_STAMPS
+    STAMP(7);
+    {
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v = lane == k ? stamp[k] : v;
+        if (a.lpc_sums && lane < 8) a.lpc_sums[gid * 32 + 24 + lane] = (long long)v;
+        if (a.fixed_sums && lane < 2) a.fixed_sums[gid * 5 + 3 + lane] = (long long)(lane ? rt1 : rt0);
+    }
+#endif
     int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
     if (lane < (1 << best)) rp[lane] = (int32_t)pkw[(lane << (oo - best)) * kRiceOrders + best];
 }
