@@ -31,6 +31,8 @@ def short(name):
 
 
 def stage(name):
+    if short(name).startswith("k_resid_stream"):  # the one-workgroup-per-unit k_resid variant
+        return "k_resid"
     for k in STAGES:
         if re.match(k + r"\b", short(name)):
             return k
