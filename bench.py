@@ -60,6 +60,9 @@ def parse(argv=None):
     ap.add_argument("--parity-units", type=int, default=64)
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-frames", action="store_true", help="skip the frame-writer measurement")
+    ap.add_argument("--e2e-units", type=int, default=100_000,
+                    help="end-to-end leg: host PCM blocks through flacmi_encode_pipeline (0 = skip)")
+    ap.add_argument("--e2e-batch", type=int, default=16384, help="end-to-end leg: units per sub-batch")
     ap.add_argument("--launch-check", action="store_true",
                     help="multi-rank plumbing only (CPU, gloo): self-launch, world-size check, shard "
                          "coverage and the stats all-reduce; prints a launch_check JSON line, no metric")
@@ -112,30 +115,104 @@ def algorithmic_bytes(cfg, meta_np, n_units):
     return lpc, resid, pipeline
 
 
+def _host_cpus():
+    """(CPU model, nproc, CPUs this process may use): the affinity mask, capped by a cgroup
+    v2 CPU quota when one is set (a GPU box shares its host between jobs)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            usable = min(usable, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return model, nproc, usable
+
+
 def cpu_baseline(cfg, seconds, seed):
     """Oracle (oracle/flac_oracle.c, a C port of the reference's hot path) on host cores,
-    on a bounded sample of the same workload; chunks of distinct synthetic units."""
+    on a bounded sample of the same workload (chunks of distinct synthetic units): every
+    CPU this process may use, and one thread."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
 
     import oracle  # test infrastructure: the CPU baseline leg only
 
-    threads = min(16, os.cpu_count() or 1)
+    model, nproc, threads = _host_cpus()
     dt = np.int16 if cfg["bits"] <= 16 else np.int32
     p = oracle.make_params(cfg["L"], cfg["q"], cfg["rmin"], cfg["rmax"], cfg["mode"])
-    chunk = 1024 if cfg["n"] <= 8192 else 128
-    done, t_an, first = 0, 0.0, 0
-    while t_an < seconds:
-        a = oracle.synth_batch(first, chunk, cfg["n"], cfg["bits"], seed, dtype=dt)
-        t0 = time.perf_counter()
-        oracle.analyze_batch(a, p, cfg["n"], sample_bits=cfg["bits"], threads=threads)
-        t_an += time.perf_counter() - t0
-        done += chunk
-        first += chunk
+
+    def run(nthreads, budget, chunk, first):
+        done, t_an = 0, 0.0
+        while t_an < budget:
+            a = oracle.synth_batch(first + done, chunk, cfg["n"], cfg["bits"], seed, dtype=dt)
+            t0 = time.perf_counter()
+            oracle.analyze_batch(a, p, cfg["n"], sample_bits=cfg["bits"], threads=nthreads)
+            t_an += time.perf_counter() - t0
+            done += chunk
+        return done, t_an
+
+    chunk = (1024 if cfg["n"] <= 8192 else 128) * max(1, threads // 16)
+    done, t_an = run(threads, seconds, chunk, 0)
+    one, t_one = run(1, max(1.0, seconds / 4), 32 if cfg["n"] <= 8192 else 4, done)
     return {"value": done * cfg["n"] / t_an, "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "nproc": nproc,
+            "one_thread": {"value": one * cfg["n"] / t_one, "unit": "samples/s",
+                           "sample": f"{one} units, {t_one:.1f} s"},
             "sample": f"{done} units x {cfg['n']} samples (synthetic units 0..{done - 1}), "
-                      f"oracle/flac_oracle.c on {threads} host threads, {t_an:.1f} s; the reference "
-                      f"Python itself measured 56.8k samples/s/core here (BASELINE.md)"}
+                      f"oracle/flac_oracle.c on {threads} host threads (the CPUs this process may use of "
+                      f"{nproc}), {t_an:.1f} s; the reference Python itself measured 56.8k samples/s/core "
+                      f"here (BASELINE.md)"}
+
+
+def end_to_end_leg(args, cfg, az):
+    """Host PCM rows -> FLAC frame bytes in host memory (end-to-end with the
+    copies reported separately): flacmi_encode_pipeline over e2e_units synthetic blocks
+    in sub-batches, the caller's buffers page-locked in place, H2D / analysis / sizes /
+    pack / D2H each timed with HIP events (they overlap across sub-batches; wall is the
+    whole call, page-locking included).  The first frames are compared with the one-shot
+    flacmi_encode_host path."""
+    import numpy as np
+    import torch
+
+    from flac_amd.analysis import make_params
+    n, bits, C = cfg["n"], cfg["bits"], cfg["channels"]
+    units = (args.e2e_units // C) * C
+    dt = torch.int16 if bits <= 16 else torch.int32
+    stride = ((n * (2 if bits <= 16 else 4) + 15) // 16) * 16 // (2 if bits <= 16 else 4)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.empty((units, stride), dtype=dt, device=dev)
+    az.synth_device(g.data_ptr(), g.element_size(), bits, stride, 10_000_000, units, n, args.seed)
+    torch.cuda.synchronize(dev)
+    host = g.cpu().numpy()
+    del g
+    params = make_params(cfg["L"], cfg["q"], cfg["rmin"], cfg["rmax"], cfg["mode"])
+    kw = dict(sample_bits=bits, channels=C, sample_size=bits, units_per_batch=args.e2e_batch)
+    az.encode_pipeline(host[: 4 * C], params, n, **kw)  # warm-up: contexts, windows, tables
+    data, offsets, status, t = az.encode_pipeline(host, params, n, **kw)
+    k = min(256, units // C)
+    ref = az.encode_frames(host[: k * C], params, n, sample_bits=bits, channels=C, sample_size=bits)
+    same = bool(np.array_equal(offsets[: k + 1], ref[1]) and
+                data[: int(offsets[k])].tobytes() == ref[0][: int(ref[1][k])].tobytes())
+    wall = t["wall_ms"]
+    return {"units": units, "samples_per_s": units * n / (wall * 1e-3), "wall_ms": wall,
+            "units_per_sub_batch": args.e2e_batch, "sub_batches": t["sub_batches"],
+            "step_ms": {k2: t[k2] for k2 in ("h2d_ms", "analyze_ms", "sizes_ms", "pack_ms", "d2h_ms", "register_ms")},
+            "h2d_GBs": t["bytes_in"] / (t["h2d_ms"] * 1e-3) / 1e9 if t["h2d_ms"] else None,
+            "d2h_GBs": t["bytes_out"] / (t["d2h_ms"] * 1e-3) / 1e9 if t["d2h_ms"] else None,
+            "bytes_in": t["bytes_in"], "bytes_out": t["bytes_out"],
+            "frames_with_status": int((status != 0).sum()),
+            "first_frames_equal_one_shot_path": same,
+            "note": "host int16 rows -> frame bytes in host memory through flacmi_encode_pipeline; "
+                    "step times are per-step sums over sub-batches (HIP events) and overlap in wall time"}
 
 
 def frame_writer_leg(args, cfg, az, samples, meta, rparams, residual, pstride, units, sptr, check):
@@ -427,6 +504,10 @@ def main(argv=None):
         frames = frame_writer_leg(args, cfg, az, samples, meta, rparams, residual, pstride, units, sptr,
                                   rank == 0 and not args.no_parity)
 
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_units > 0 and not chunked:
+        e2e = end_to_end_leg(args, cfg, az)
+
     lpc_b, resid_b, pipe_b = algorithmic_bytes(cfg, meta_np, units)
     lpc_gbs = lpc_b / (kt["lpc_ms"] * 1e-3) / 1e9 if kt["lpc_ms"] > 0 else 0.0
     resid_gbs = resid_b / (kt["resid_ms"] * 1e-3) / 1e9 if kt["resid_ms"] > 0 else 0.0
@@ -469,6 +550,7 @@ def main(argv=None):
                         "timed_calls": kt["calls"]},
             "cpu_baseline": cpu,
             "frame_writer": frames,
+            "end_to_end": e2e,
             "parity": parity,
             "stream_stats": {"units": int(st[0]), "samples": int(st[1]), "rice_bits": int(st[2]),
                              "fixed": int(st[3]), "lpc": int(st[4]), "errors": int(st[65:80].sum())},

@@ -9,9 +9,11 @@ import numpy as np
 
 ABI_VERSION = 1
 MAX_LPC_ORDER = 32
-MAX_BLOCK = 32768
+MAX_BLOCK = 65535
 MAX_RICE_ORDER = 15
 STATS_WORDS = 128
+# flacmi_error
+E_INVALID, E_HIP, E_UNSUPPORTED, E_NOMEM = -1, -2, -3, -4
 
 
 def lpc_rec_words(L: int) -> int:
@@ -153,6 +155,21 @@ class FrameParams(C.Structure):
     ]
 
 
+class EncodeTiming(C.Structure):
+    _fields_ = [
+        ("wall_ms", C.c_double),
+        ("h2d_ms", C.c_double),
+        ("analyze_ms", C.c_double),
+        ("sizes_ms", C.c_double),
+        ("pack_ms", C.c_double),
+        ("d2h_ms", C.c_double),
+        ("register_ms", C.c_double),
+        ("sub_batches", C.c_int64),
+        ("bytes_in", C.c_int64),
+        ("bytes_out", C.c_int64),
+    ]
+
+
 class DecodeParams(C.Structure):
     _fields_ = [
         ("channels", C.c_int32),
@@ -191,6 +208,9 @@ SIGNATURES = {
     "flacmi_encode_host": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Params), C.POINTER(FrameParams),
                                      C.c_void_p, C.c_void_p]),
     "flacmi_encode_fetch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "flacmi_encode_pipeline": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Params), C.POINTER(FrameParams),
+                                         C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                         C.POINTER(EncodeTiming)]),
     "flacmi_decode_frames_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                               C.POINTER(DecodeParams), C.POINTER(Batch), C.c_void_p, C.c_int64,
                                               C.c_void_p, C.c_void_p, C.c_void_p]),

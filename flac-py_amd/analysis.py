@@ -181,6 +181,48 @@ class Analyzer:
         check(self.lib.flacmi_encode_fetch(self.ctx, out.ctypes.data, total), "flacmi_encode_fetch")
         return out, offsets, status[:n_frames]
 
+    def encode_pipeline(self, samples: np.ndarray, params: abi.Params, block_len: int, tail_len: int = 0,
+                        n_tail_units: int = 0, sample_bits: int = 16, channels: int = 1, sample_size: int = 16,
+                        first_frame: int = 0, units_per_batch: int = 8192, capacity: int = 0):
+        """encode_frames through flacmi_encode_pipeline: host rows in (any row stride), the
+        batch streamed through the device in sub-batches of units_per_batch units with the
+        PCIe copies overlapping the kernels.  Returns (frame bytes, frame offsets
+        [n_frames + 1], frame status [n_frames], timing dict)."""
+        s = samples
+        if s.dtype not in (np.int16, np.int32) or s.ndim != 2 or s.strides[1] != s.itemsize:
+            raise ValueError("samples must be a 2-D int16 or int32 array with contiguous rows")
+        if s.strides[0] % s.itemsize:
+            raise ValueError("the row stride must be a whole number of samples")
+        n_units = s.shape[0]
+        b = abi.Batch()
+        b.samples = s.ctypes.data
+        b.sample_bytes = s.itemsize
+        b.sample_bits = sample_bits
+        b.unit_stride = s.strides[0] // s.itemsize
+        b.n_units = n_units
+        b.block_len = block_len
+        b.tail_len = tail_len
+        b.n_tail_units = n_tail_units
+        fp = frame_params(channels, sample_size, params.qlp_precision, first_frame)
+        n_frames = n_units // channels if channels else 0
+        offsets = np.zeros(n_frames + 1, dtype=np.int64)
+        status = np.zeros(max(n_frames, 1), dtype=np.int32)
+        upb = max(channels, (units_per_batch // channels) * channels)
+        cap = capacity or int(n_units * (block_len * s.itemsize * 1.25 + 256)) + (1 << 20)
+        while True:
+            out = np.empty(cap, dtype=np.uint8)
+            t = abi.EncodeTiming()
+            rc = self.lib.flacmi_encode_pipeline(self.ctx, C.byref(b), C.byref(params), C.byref(fp), upb,
+                                                 out.ctypes.data, cap, offsets.ctypes.data, status.ctypes.data,
+                                                 C.byref(t))
+            if rc == abi.E_NOMEM and not capacity:
+                cap *= 2
+                continue
+            check(rc, "flacmi_encode_pipeline")
+            break
+        timing = {f: getattr(t, f) for f, _ in abi.EncodeTiming._fields_}
+        return out[:int(offsets[-1])], offsets, status[:n_frames], timing
+
     def frame_sizes_device(self, batch: abi.Batch, fp: abi.FrameParams, meta_ptr: int, params_ptr: int,
                            params_stride: int, offsets_ptr: int, status_ptr: int, stream: int = 0) -> None:
         check(self.lib.flacmi_frame_sizes_device(self.ctx, C.byref(batch), C.byref(fp), meta_ptr, params_ptr,

@@ -13,7 +13,9 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cerrno>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -848,6 +850,233 @@ int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_
         ctx->frames_bytes = total;
         return 0;
     }
+}
+
+/* ---- pipelined host encode ---------------------------------------------------------
+ * Streams: `cs` (compute: analysis, sizes, pack, in order, so the context's shared scratch
+ * is never used by two launches at once), `is` (host -> device) and `os` (device -> host).
+ * Per sub-batch k (slot k % kEncSlots):
+ *   front(k): is: H2D rows -> cs: analyze, frame sizes -> os: offsets/status D2H (pinned)
+ *   back(k):  host waits for those offsets, then cs: pack -> os: frame bytes D2H into out
+ * issued as front(0), front(1), back(0), front(2), back(1), ... so the copies of one
+ * sub-batch run under the kernels of the others. */
+namespace {
+struct EncSlot {
+    DevBuf samples, meta, params, residual, offsets, status, frames;
+    int64_t* h_off = nullptr;   /* pinned: frame offsets of the sub-batch */
+    int32_t* h_st = nullptr;    /* pinned: frame status */
+    hipEvent_t e[9] = {};       /* h2d start/end, analyze end, sizes end, pack start/end, d2h start/end, offsets copied */
+    flacmi_batch b{};
+    int64_t first_unit = 0, nf = 0, total = 0;
+    int rbytes = 4;
+};
+float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.0f;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.0f;
+}
+}  // namespace
+
+static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, const flacmi_params* params,
+                     const flacmi_frame_params* fp, hipStream_t cs, hipStream_t is, hipStream_t os) {
+    const flacmi_batch& b = sl.b;
+    const size_t nu = (size_t)b.n_units;
+    const int64_t sstride = ((b.block_len * b.sample_bytes + 15) / 16) * 16 / b.sample_bytes;
+    const int64_t pstride = (1LL << (params->rice_max > 0 ? params->rice_max : 0)) + 1;
+    const int64_t rstride = ((b.block_len * sl.rbytes + 15) / 16) * 16 / sl.rbytes;
+    if (int rc = ensure_buf(sl.samples, nu * sstride * b.sample_bytes)) return rc;
+    if (int rc = ensure_buf(sl.meta, nu * sizeof(flacmi_unit_meta))) return rc;
+    if (int rc = ensure_buf(sl.params, nu * pstride * sizeof(int32_t))) return rc;
+    if (int rc = ensure_buf(sl.residual, nu * rstride * sl.rbytes)) return rc;
+    if (int rc = ensure_buf(sl.offsets, sizeof(int64_t) * (size_t)(sl.nf + 1))) return rc;
+    if (int rc = ensure_buf(sl.status, sizeof(int32_t) * (size_t)sl.nf)) return rc;
+    HIP_TRY(hipEventRecord(sl.e[0], is));
+    HIP_TRY(hipMemcpy2DAsync(sl.samples.p, sstride * b.sample_bytes,
+                             (const uint8_t*)whole->samples + sl.first_unit * whole->unit_stride * b.sample_bytes,
+                             whole->unit_stride * b.sample_bytes, b.block_len * b.sample_bytes, nu,
+                             hipMemcpyHostToDevice, is));
+    HIP_TRY(hipEventRecord(sl.e[1], is));
+    HIP_TRY(hipStreamWaitEvent(cs, sl.e[1], 0));
+    flacmi_batch db = b;
+    db.samples = sl.samples.p;
+    db.unit_stride = sstride;
+    flacmi_outputs o{};
+    o.meta = (flacmi_unit_meta*)sl.meta.p;
+    o.rice_params = (int32_t*)sl.params.p;
+    o.params_stride = pstride;
+    o.residual = sl.residual.p;
+    o.residual_bytes = sl.rbytes;
+    o.residual_stride = rstride;
+    if (int rc = validate(&db, params, &o)) return rc;
+    if (int rc = analyze_device_impl(ctx, &db, params, &o, cs)) return rc;
+    HIP_TRY(hipEventRecord(sl.e[2], cs));
+    flacmi_frame_params f = *fp;
+    f.first_frame = fp->first_frame + sl.first_unit / fp->channels;
+    FrameArgs a = frame_args(ctx, &db, &f, o.meta, o.rice_params, pstride, sl.nf);
+    if (int rc = frame_sizes_impl(ctx, a, (int64_t*)sl.offsets.p, (int32_t*)sl.status.p, cs)) return rc;
+    HIP_TRY(hipEventRecord(sl.e[3], cs));
+    HIP_TRY(hipStreamWaitEvent(os, sl.e[3], 0));
+    HIP_TRY(hipMemcpyAsync(sl.h_off, sl.offsets.p, sizeof(int64_t) * (sl.nf + 1), hipMemcpyDeviceToHost, os));
+    HIP_TRY(hipMemcpyAsync(sl.h_st, sl.status.p, sizeof(int32_t) * sl.nf, hipMemcpyDeviceToHost, os));
+    HIP_TRY(hipEventRecord(sl.e[8], os));
+    return 0;
+}
+
+extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_params* params,
+                                      const flacmi_frame_params* fp, int64_t units_per_batch, uint8_t* out,
+                                      int64_t out_capacity, int64_t* frame_offsets, int32_t* frame_status,
+                                      flacmi_encode_timing* timing) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
+    int64_t nf = 0;
+    if (int rc = validate_frames(batch, fp, &nf)) return rc;
+    if (!params || !frame_offsets || !frame_status || (!out && out_capacity > 0))
+        return fail(FLACMI_E_INVALID, "null argument");
+    const int C = fp->channels;
+    if (units_per_batch < C || units_per_batch % C) return fail(FLACMI_E_INVALID, "units_per_batch must be a positive multiple of channels");
+    if (batch->unit_stride < batch->block_len) return fail(FLACMI_E_INVALID, "unit_stride < block_len");
+    flacmi_encode_timing t{};
+    const auto w0 = std::chrono::steady_clock::now();
+    frame_offsets[0] = 0;
+    if (nf == 0) {
+        if (timing) *timing = t;
+        return 0;
+    }
+    if (int rc = set_device(ctx)) return rc;
+    /* the caller's rows and output, page-locked in place for the call */
+    const auto r0 = std::chrono::steady_clock::now();
+    const size_t in_bytes = (size_t)((batch->n_units - 1) * batch->unit_stride + batch->block_len) * batch->sample_bytes;
+    const bool reg_in = hipHostRegister(const_cast<void*>(batch->samples), in_bytes, hipHostRegisterDefault) == hipSuccess;
+    const bool reg_out = out_capacity > 0 && hipHostRegister(out, (size_t)out_capacity, hipHostRegisterDefault) == hipSuccess;
+    (void)hipGetLastError();
+    t.register_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
+    constexpr int kEncSlots = 3;
+    hipStream_t cs = nullptr, is = nullptr, os = nullptr;
+    EncSlot slot[kEncSlots];
+    int rc = 0;
+    auto cleanup = [&]() {
+        for (hipStream_t st : {cs, is, os})
+            if (st) (void)hipStreamSynchronize(st);
+        for (auto& sl : slot) {
+            for (DevBuf* d : {&sl.samples, &sl.meta, &sl.params, &sl.residual, &sl.offsets, &sl.status, &sl.frames})
+                if (d->p) (void)hipFree(d->p);
+            if (sl.h_off) (void)hipHostFree(sl.h_off);
+            if (sl.h_st) (void)hipHostFree(sl.h_st);
+            for (auto& e : sl.e)
+                if (e) (void)hipEventDestroy(e);
+        }
+        for (hipStream_t st : {cs, is, os})
+            if (st) (void)hipStreamDestroy(st);
+        const auto u0 = std::chrono::steady_clock::now();
+        if (reg_in) (void)hipHostUnregister(const_cast<void*>(batch->samples));
+        if (reg_out) (void)hipHostUnregister(out);
+        t.register_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
+    };
+#define ENC_TRY(x)                                                                        \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            rc = fail(FLACMI_E_HIP, "%s: %s", #x, hipGetErrorString(e_));                 \
+            goto done;                                                                    \
+        }                                                                                 \
+    } while (0)
+    {
+        ENC_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        ENC_TRY(hipStreamCreateWithFlags(&is, hipStreamNonBlocking));
+        ENC_TRY(hipStreamCreateWithFlags(&os, hipStreamNonBlocking));
+        const int64_t per_nf = units_per_batch / C;
+        for (auto& sl : slot) {
+            ENC_TRY(hipHostMalloc((void**)&sl.h_off, sizeof(int64_t) * (per_nf + 1), hipHostMallocDefault));
+            ENC_TRY(hipHostMalloc((void**)&sl.h_st, sizeof(int32_t) * per_nf, hipHostMallocDefault));
+            for (auto& e : sl.e) ENC_TRY(hipEventCreate(&e));
+        }
+        const int64_t nsub = (batch->n_units + units_per_batch - 1) / units_per_batch;
+        auto setup = [&](int64_t k) {
+            EncSlot& sl = slot[k % kEncSlots];
+            sl.first_unit = k * units_per_batch;
+            const int64_t nu = std::min(units_per_batch, batch->n_units - sl.first_unit);
+            sl.b = *batch;
+            sl.b.n_units = nu;
+            sl.b.n_tail_units = (sl.first_unit + nu == batch->n_units) ? batch->n_tail_units : 0;
+            sl.nf = nu / C;
+            sl.rbytes = 4;
+        };
+        int64_t written = 0; /* frame bytes of the sub-batches already placed */
+        auto back = [&](int64_t k) -> int {
+            EncSlot& sl = slot[k % kEncSlots];
+            HIP_TRY(hipEventSynchronize(sl.e[8])); /* the offsets / status of sub-batch k */
+            bool wide = false;
+            for (int64_t f = 0; f < sl.nf && sl.rbytes == 4; ++f)
+                if ((sl.h_st[f] & 0xffff) == FLACMI_STATUS_RESIDUAL_WIDE) wide = true;
+            if (wide) { /* a chosen residual needs 64 bits: redo this sub-batch with 8-byte rows */
+                sl.rbytes = 8;
+                if (int r = enc_front(ctx, sl, batch, params, fp, cs, is, os)) return r;
+                HIP_TRY(hipEventSynchronize(sl.e[8]));
+            }
+            sl.total = sl.h_off[sl.nf];
+            const int64_t f0 = sl.first_unit / C;
+            for (int64_t f = 0; f < sl.nf; ++f) {
+                frame_offsets[f0 + f + 1] = written + sl.h_off[f + 1];
+                frame_status[f0 + f] = sl.h_st[f];
+            }
+            if (written + sl.total > out_capacity)
+                return fail(FLACMI_E_NOMEM, "frames need %lld bytes, out holds %lld", (long long)(written + sl.total),
+                            (long long)out_capacity);
+            if (int r = ensure_buf(sl.frames, (size_t)sl.total + 16)) return r;
+            const int64_t pstride = (1LL << (params->rice_max > 0 ? params->rice_max : 0)) + 1;
+            const int64_t sstride = ((sl.b.block_len * sl.b.sample_bytes + 15) / 16) * 16 / sl.b.sample_bytes;
+            const int64_t rstride = ((sl.b.block_len * sl.rbytes + 15) / 16) * 16 / sl.rbytes;
+            flacmi_batch db = sl.b;
+            db.samples = sl.samples.p;
+            db.unit_stride = sstride;
+            flacmi_frame_params f = *fp;
+            f.first_frame = fp->first_frame + f0;
+            FrameArgs a = frame_args(ctx, &db, &f, (const flacmi_unit_meta*)sl.meta.p, (const int32_t*)sl.params.p,
+                                     pstride, sl.nf);
+            a.residual = sl.residual.p;
+            a.residual_bytes = sl.rbytes;
+            a.residual_stride = rstride;
+            a.offsets = (int64_t*)sl.offsets.p;
+            a.status = (int32_t*)sl.status.p;
+            a.out = (uint8_t*)sl.frames.p;
+            a.capacity = sl.total;
+            if (int r = pack_lists(ctx, a)) return r;
+            HIP_TRY(hipEventRecord(sl.e[4], cs));
+            HIP_TRY(launch_pack(a, cs));
+            HIP_TRY(hipEventRecord(sl.e[5], cs));
+            HIP_TRY(hipStreamWaitEvent(os, sl.e[5], 0));
+            HIP_TRY(hipEventRecord(sl.e[6], os));
+            if (sl.total > 0)
+                HIP_TRY(hipMemcpyAsync(out + written, sl.frames.p, (size_t)sl.total, hipMemcpyDeviceToHost, os));
+            HIP_TRY(hipEventRecord(sl.e[7], os));
+            written += sl.total;
+            t.bytes_out += sl.total;
+            return 0;
+        };
+        auto account = [&](int64_t k) {
+            EncSlot& sl = slot[k % kEncSlots];
+            (void)hipEventSynchronize(sl.e[7]);
+            t.h2d_ms += ev_ms(sl.e[0], sl.e[1]);
+            t.analyze_ms += ev_ms(sl.e[1], sl.e[2]);
+            t.sizes_ms += ev_ms(sl.e[2], sl.e[3]);
+            t.pack_ms += ev_ms(sl.e[4], sl.e[5]);
+            t.d2h_ms += ev_ms(sl.e[6], sl.e[7]);
+            t.bytes_in += (int64_t)sl.b.n_units * sl.b.block_len * sl.b.sample_bytes;
+        };
+        for (int64_t k = 0; k < nsub; ++k) {
+            if (k >= kEncSlots) account(k - kEncSlots); /* the slot is free once those frames are copied */
+            setup(k);
+            if ((rc = enc_front(ctx, slot[k % kEncSlots], batch, params, fp, cs, is, os))) goto done;
+            if (k >= 1 && (rc = back(k - 1))) goto done;
+        }
+        if ((rc = back(nsub - 1))) goto done;
+        for (int64_t k = (nsub >= kEncSlots ? nsub - kEncSlots : 0); k < nsub; ++k) account(k);
+        t.sub_batches = nsub;
+    }
+done:
+#undef ENC_TRY
+    cleanup();
+    t.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+    if (timing) *timing = t;
+    return rc;
 }
 
 int flacmi_encode_fetch(flacmi_ctx* ctx, uint8_t* out, int64_t bytes) {

@@ -27,6 +27,9 @@
  * use one context per host thread.  The *_device entry points take device pointers
  * and enqueue on the given hipStream_t (passed as void*), returning without a host
  * synchronisation; the *_host entry points take host pointers and are synchronous.
+ * The *_device calls of one context share its scratch buffers (LPC records, retry and
+ * pack lists, decoder state): issue them on one stream, or make each call's stream
+ * wait for the previous call's work, never concurrently on two streams.
  */
 #ifndef FLACMI_H
 #define FLACMI_H
@@ -40,7 +43,9 @@ extern "C" {
 
 #define FLACMI_ABI_VERSION 1
 #define FLACMI_MAX_LPC_ORDER 32      /* EncoderParameters: lpc_order.stop <= 33 (encoder.py:42) */
-#define FLACMI_MAX_BLOCK 32768       /* largest block size flac-py encodes (common.py BLOCK_SIZE_ENCODING) */
+#define FLACMI_MAX_BLOCK 65535       /* largest block the reference writes (encoder.py:249-253, 16-bit uncommon
+                                        code); analysis returns FLACMI_E_UNSUPPORTED where a block's
+                                        workgroup staging exceeds LDS (above ~16K samples) */
 #define FLACMI_MAX_RICE_ORDER 15     /* 4-bit partition-order field (encoder.py:767) */
 #define FLACMI_LPC_REC_WORDS(L) (2 + (L) + ((L) * ((L) + 1)) / 2)
 
@@ -232,6 +237,33 @@ int flacmi_pack_frames_device(flacmi_ctx* ctx, const flacmi_batch* batch, const 
 int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_params* params,
                        const flacmi_frame_params* fp, int64_t* frame_offsets, int32_t* frame_status);
 int flacmi_encode_fetch(flacmi_ctx* ctx, uint8_t* out, int64_t bytes);
+
+/* Pipelined host encode (SURVEY §8d end-to-end; the reference's encode() loop plus its
+ * writer, encoder.py:87-165, 765-806): host sample rows in, FLAC frame bytes out, the batch
+ * cut into sub-batches of units_per_batch units (a multiple of channels) with two in
+ * flight: the copy of sub-batch k+1 to the device and its analysis overlap the frame
+ * writing and the copy back of sub-batch k.  The caller's sample rows and `out` are
+ * page-locked in place for the call (hipHostRegister) so both copies are DMA at PCIe rate.
+ * out receives the frames back to back; frame_offsets[n_frames + 1] their byte offsets and
+ * frame_status[n_frames] as flacmi_frame_sizes_device (a failing frame has no bytes).
+ * FLACMI_E_NOMEM if the frames exceed out_capacity (frame_offsets then hold the sizes of
+ * the sub-batches written so far).  timing (optional) receives per-step times. */
+typedef struct flacmi_encode_timing {
+    double wall_ms;        /* the whole call */
+    double h2d_ms;         /* sum over sub-batches of each step's own duration (HIP events): */
+    double analyze_ms;     /*   host -> device sample copy, analysis (k_lpc + k_resid), */
+    double sizes_ms;       /*   frame sizes + scan, frame writing (k_pack32 / k_pack), */
+    double pack_ms;        /*   device -> host frame copy; the steps of different */
+    double d2h_ms;         /*   sub-batches overlap in wall time */
+    double register_ms;    /* hipHostRegister / Unregister of the caller's buffers */
+    int64_t sub_batches;
+    int64_t bytes_in;      /* sample bytes copied to the device */
+    int64_t bytes_out;     /* frame bytes copied back */
+} flacmi_encode_timing;
+int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_params* params,
+                           const flacmi_frame_params* fp, int64_t units_per_batch, uint8_t* out,
+                           int64_t out_capacity, int64_t* frame_offsets, int32_t* frame_status,
+                           flacmi_encode_timing* timing);
 
 /* ---- decoder verifier (BASELINE config 5 round trip) ------------- */
 /* Replaces the reference's frame decoder: decoder.py:111-130 get_frame, :133-190

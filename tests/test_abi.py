@@ -34,7 +34,8 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
     structs = {"flacmi_params": abi.Params, "flacmi_batch": abi.Batch,
                "flacmi_unit_meta": abi.UnitMeta, "flacmi_outputs": abi.Outputs,
-               "flacmi_frame_params": abi.FrameParams, "flacmi_decode_params": abi.DecodeParams}
+               "flacmi_frame_params": abi.FrameParams, "flacmi_decode_params": abi.DecodeParams,
+               "flacmi_encode_timing": abi.EncodeTiming}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

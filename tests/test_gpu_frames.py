@@ -131,3 +131,28 @@ def test_general_writer_alone_matches(az, name, monkeypatch):
                            first_frame=first)
     assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2])
     assert got[0].tobytes() == want[0].tobytes()
+
+
+@pytest.mark.parametrize("name,upb", [("c2", 5), ("c1_tail", 4), ("c3_stereo", 2), ("bs16_3ch", 3),
+                                      ("q16_assert", 12), ("wide20", 4), ("big3ch_list", 6)])
+def test_encode_pipeline_equals_encode_frames(az, name, upb):
+    """flacmi_encode_pipeline (sub-batches of upb frames, three in flight, the caller's
+    buffers page-locked in place) gives the bytes, offsets and statuses of the one-shot
+    flacmi_encode_host path, including the short last frame, the writer's own asserts
+    and the 64-bit-residual redo; the rows are a strided view (row stride > block)."""
+    frames, C, n, tail, bits, L, q, rmin, rmax, mode, ss, first, seed = CASES[name]
+    rows, n_tail = _rows(frames, C, n, tail, bits, seed)
+    params = oracle.make_params(L, q, rmin, rmax, mode)
+    want = az.encode_frames(rows, params, n, tail, n_tail, sample_bits=bits, channels=C, sample_size=ss,
+                            first_frame=first)
+    wide = np.zeros((rows.shape[0], n + 40), dtype=rows.dtype)
+    wide[:, :n] = rows
+    view = wide[:, :n]  # row stride n + 40 samples
+    data, offsets, status, timing = az.encode_pipeline(view, params, n, tail, n_tail, sample_bits=bits,
+                                                       channels=C, sample_size=ss, first_frame=first,
+                                                       units_per_batch=upb * C)
+    assert np.array_equal(offsets, want[1]), name
+    assert np.array_equal(status, want[2]), name
+    assert data.tobytes() == want[0].tobytes(), name
+    assert timing["sub_batches"] == (frames + upb - 1) // upb
+    assert timing["bytes_out"] == int(offsets[-1])

@@ -308,3 +308,17 @@ def test_large_residuals_chunked_rice_bits(az, mode):
     ora = oracle.analyze_batch(a, oracle.make_params(L, 12, 0, 8, mode), n, sample_bits=32, threads=16)
     assert int((ora["meta"]["status"] == 0).sum()) >= nu // 2
     compare_with_oracle(out, ora, [n] * nu)
+
+
+def test_long_blocks_are_declared_unsupported(az):
+    """The reference writes blocks up to 65535 samples (16-bit uncommon block-size code,
+    encoder.py:249-253); the API accepts them, and a block whose workgroup staging exceeds
+    the 160 KB LDS is refused with FLACMI_E_UNSUPPORTED naming the LDS need,
+    never with E_INVALID and never by a failed launch."""
+    from flac_amd._lib import FlacmiError
+    params = make_params(8, 5, 0, 5)
+    for n in (40000, 65535):
+        rows = np.zeros((1, ((n * 2 + 15) // 16) * 8), dtype=np.int16)
+        with pytest.raises(FlacmiError) as ei:
+            az.analyze(rows, params, n)
+        assert f"({abi.E_UNSUPPORTED})" in str(ei.value) and "LDS" in str(ei.value)
