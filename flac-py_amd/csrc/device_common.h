@@ -193,9 +193,11 @@ __host__ __device__ inline int resid_xpad(int n) {
     return a > b ? a : b;
 }
 
-/* MFMA candidate-sum planes (k_resid, S16 path): bf16 high / low sample bytes, elements
- * [-16, len - 16) per plane. */
-__host__ __device__ inline int mfma_plane_len(int n) { return ((n + 63) / 64) * 64 + 32; }
+/* int8-MFMA candidate-sum planes (k_resid, PATH_W64): three byte planes of the samples'
+ * balanced base-256 digits, sample i at byte kMf8Pad + i of its plane, zero outside
+ * [0, n); the 16-byte tail keeps every 5-dword fragment read inside the plane. */
+constexpr int kMf8Pad = 32;
+__host__ __device__ inline int mf8_plane_bytes(int n) { return ((n + kMf8Pad + 16) + 15) & ~15; }
 
 struct ResidLds {
     int xs, pl, zz, cs, coef, red, dec, rb, misc, hs, hp, tl, total;
@@ -213,7 +215,7 @@ __host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, in
     l.xs = o;   o = up(o + xbytes * (resid_hp(lmax) + resid_xpad(n)));
     /* the MFMA planes are dead after the candidate sums; the residual-side regions reuse them */
     l.pl = o;
-    const int pl_end = up(o + (planes ? 2 * 2 * mfma_plane_len(n) : 0));
+    const int pl_end = up(o + (planes ? 3 * mf8_plane_bytes(n) : 0));
     l.zz = o;   o = up(o + (regz ? 0 : zbytes * npad)); /* zig-zag row (LDS-resident mode) */
     l.cs = o;   o = up(o + (regz ? 4 * (npad / 8) : 0)); /* chunk sums (register-resident mode) */
     l.hs = o;   o = up(o + 8 * 2 * P);

@@ -491,6 +491,195 @@ __device__ __forceinline__ void mfma_candidate_sums(const int16_t* xs16, const f
     if (lane == 0) red[wid * NSUM] = sx;
 }
 
+/* ---------------------------------------------------------------------------------------
+ * int8-MFMA candidate sums (PATH_W64, L <= 32, samples <= 24 bits, |c| < 2^15 - 128):
+ * the prediction_residual loops of encoder.py:537-548 for all L orders at once, as
+ * v_mfma_i32_16x16x64_i8 over Toeplitz windows of byte digits.
+ *
+ * Digits (balanced base 256): x = b0 + 2^8 b1 + 2^16 b2, c = e0 + 2^8 e1, every digit a
+ * signed byte (b2 <= 127 holds for x <= 8355711: checked per unit).  The six digit products
+ * are grouped by weight: P_w = sum over d + e = w of sum_j b_d[i-1-j] e_e[c_j], w = 0..3, one
+ * MFMA each, |P_w| <= 64 * 2^14 = 2^20.  Then pred = 2^16 (P2 + 2^8 P3) + (P0 + 2^8 P1)
+ * with lo = P0 + 2^8 P1 exact in int32, so for any shift s <= 15
+ *     floor(pred / 2^s) = ((P2 + 2^8 P3) << (16 - s)) + (lo >> s)      (mod 2^32)
+ * exactly, and |r| = |floor(pred / 2^s) - x|.  P2's accumulator starts at 2^(15+s), which
+ * adds 2^31 to the result: against x ^ 2^31 one v_sad_u32 gives |r| whenever the true
+ * floor(pred/2^s) and x lie in [-2^31, 2^31); the unit's bound B = max|x| + max_p
+ * (sum|c_p| max|x| >> s_p) + 1 < 2^30 guarantees it (checked per unit, with the number of
+ * tiles G whose 4 values per lane a u32 partial sum can hold).  Per sample and order: 5 VALU
+ * (two shift-adds, one shift, one shift-add, one sad) instead of p v_mad_i64_i32.
+ *
+ * Tile = 16 samples i0..i0+15 (MFMA rows), N-tile nt = orders 16nt+1 .. 16nt+16 (columns).
+ * Lane l: row m = l & 15, K quarter qq = l >> 4, slot sg = qq >> 1, half h = qq & 1; its 16
+ * K bytes are taps j = 16h + 15 - t (t = 0..15), i.e. the 16 samples from i0 + m - 16 - 16h
+ * upward: one unaligned 16-byte window of a digit plane (5 dword reads, 4 v_alignbyte).
+ * Slot 0 carries (b0,e0) (b1,e0) (b2,e0) (b2,e1) for P0..P3, slot 1 (b0,e1) (b1,e1) for P1, P2.
+ * tools/check_mfma_i8.hip pins the operand layout on gfx950.
+ * ------------------------------------------------------------------------------------- */
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int32_t sext8(int32_t v) { return (int32_t)(int8_t)(v & 255); }
+
+/* balanced base-256 digits of an int32 sample (b2 in [-128, 128]: 128 only above 8355711) */
+__device__ __forceinline__ void mf8_digits(int32_t x, int32_t& b0, int32_t& b1, int32_t& b2) {
+    b0 = sext8(x);
+    const int32_t x1 = (x - b0) >> 8;
+    b1 = sext8(x1);
+    b2 = (x1 - b1) >> 8;
+}
+
+/* 16 plane bytes from byte offset o (any alignment) */
+__device__ __forceinline__ v4i mf8_frag(const uint32_t* pw, int o) {
+    const int dw = o >> 2;
+    const uint32_t sh = (uint32_t)(o & 3);
+    const uint32_t d0 = pw[dw], d1 = pw[dw + 1], d2 = pw[dw + 2], d3 = pw[dw + 3], d4 = pw[dw + 4];
+    v4i r;
+    r[0] = (int)__builtin_amdgcn_alignbyte(d1, d0, sh);
+    r[1] = (int)__builtin_amdgcn_alignbyte(d2, d1, sh);
+    r[2] = (int)__builtin_amdgcn_alignbyte(d3, d2, sh);
+    r[3] = (int)__builtin_amdgcn_alignbyte(d4, d3, sh);
+    return r;
+}
+
+/* one 16-sample tile for N-tile operands B*, accumulating |r| of the lane's column into s32 */
+template <bool MASK>
+__device__ __forceinline__ void mf8_tile_epilogue(const v4i (&D)[4], int s, const uint32_t (&xb)[4], int i0r,
+                                                  int start, uint32_t& s32) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int32_t lo = (int32_t)((uint32_t)D[0][r] + ((uint32_t)D[1][r] << 8));
+        const int32_t hi = (int32_t)((uint32_t)D[2][r] + ((uint32_t)D[3][r] << 8));
+        const uint32_t t = ((uint32_t)hi << (16 - s)) + (uint32_t)(lo >> s);
+        if constexpr (MASK) {
+            const uint32_t v = sad_u32(t, xb[r], 0u);
+            s32 += (i0r + r >= start) ? v : 0u;
+        } else {
+            s32 = sad_u32(t, xb[r], s32);
+        }
+    }
+}
+
+/* Sums of |r| for LPC orders 1..L (into red[wid][5 + p - 1]) and fixed orders 0..4 (VALU,
+ * 8-sample chunks, into red[wid][0..4]).  pl: the three digit planes, PLB bytes apart;
+ * cfl / lsh: phase A's coefficient and shift tables; G: tiles per u32 partial sum. */
+template <int LMAX>
+__device__ __forceinline__ void mf8_candidate_sums(const int32_t* xs32, const unsigned char* pl, int PLB,
+                                                   const int32_t* cfl, const int32_t* lsh, int L, int n, int G,
+                                                   int tid, int NT, int lane, int wid, int nw,
+                                                   unsigned long long* red) {
+    using CT = CoefTables<LMAX>;
+    constexpr int NSUM = 5 + LMAX;
+    constexpr int NTMAX = (LMAX + 15) / 16;
+    /* fixed orders on the VALU */
+    {
+        uint64_t fa[5] = {0, 0, 0, 0, 0};
+        const int nch = n >> 3;
+#pragma unroll 1
+        for (int c = tid; c < nch; c += NT) {
+            const int i0 = 8 * c;
+            int32_t x12[12];
+            const int4v* src = reinterpret_cast<const int4v*>(xs32 + i0 - 4);
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                const int4v v = src[g];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x12[4 * g + e] = v[e];
+            }
+            if (i0 >= 8) fixed_sums32<false>(x12, i0, n, fa);
+            else fixed_sums32<true>(x12, i0, n, fa);
+        }
+#pragma unroll
+        for (int o = 0; o < 5; ++o) {
+            const uint64_t v = wave_sum_u64(fa[o]);
+            if (lane == 0) red[wid * NSUM + o] = v;
+        }
+    }
+    const int col = lane & 15, qq = lane >> 4, sg = qq >> 1, h = qq & 1, m = col;
+    const int nt_live = L > 16 ? 2 : 1;
+    /* B operands and per-column constants */
+    v4i Bw0[NTMAX], Bx[NTMAX], Bw3[NTMAX], C2[NTMAX];
+    int sh[NTMAX], st[NTMAX];
+#pragma unroll
+    for (int nt = 0; nt < NTMAX; ++nt) {
+        const int p = 16 * nt + col + 1;
+        const bool live = p <= L;
+        uint32_t w0[4] = {0, 0, 0, 0}, wx[4] = {0, 0, 0, 0}, w3[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int j = 16 * h + 15 - t;
+            const int32_t c = (live && j < p) ? cfl[(p - 1) * CT::CPAD + j] : 0;
+            const int32_t e0 = sext8(c), e1 = (c - e0) >> 8;
+            const uint32_t bx = (uint32_t)(sg == 0 ? e0 : e1) & 255u;
+            const uint32_t b0 = sg == 0 ? (uint32_t)e0 & 255u : 0u;
+            const uint32_t b3 = sg == 0 ? (uint32_t)e1 & 255u : 0u;
+            wx[t >> 2] |= bx << (8 * (t & 3));
+            w0[t >> 2] |= b0 << (8 * (t & 3));
+            w3[t >> 2] |= b3 << (8 * (t & 3));
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            Bw0[nt][g] = (int)w0[g];
+            Bx[nt][g] = (int)wx[g];
+            Bw3[nt][g] = (int)w3[g];
+        }
+        sh[nt] = live ? lsh[p - 1] : 0;
+        st[nt] = live ? lsh[LMAX + p - 1] : 0x7fffffff;
+        const int cb = (int)(1u << (15 + sh[nt]));
+        C2[nt] = v4i{cb, cb, cb, cb};
+    }
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(pl);
+    const int off0 = kMf8Pad + m - 16 - 16 * h;
+    const int off1 = off0 + (sg == 0 ? PLB : 0);
+    const int off2 = off0 + (sg == 0 ? 2 * PLB : PLB);
+    const v4i Z{0, 0, 0, 0};
+    uint64_t acc[NTMAX];
+    uint32_t s32[NTMAX];
+#pragma unroll
+    for (int nt = 0; nt < NTMAX; ++nt) acc[nt] = 0, s32[nt] = 0;
+    const int ntile = n >> 4;
+    auto tile = [&](int T, auto MASK_) __attribute__((always_inline)) {
+        constexpr bool MASK = decltype(MASK_)::value;
+        const int i0 = T << 4;
+        const v4i A0 = mf8_frag(pw, off0 + i0), A1 = mf8_frag(pw, off1 + i0), A2 = mf8_frag(pw, off2 + i0);
+        const int4v xv = *reinterpret_cast<const int4v*>(xs32 + i0 + 4 * qq);
+        const uint32_t xb[4] = {(uint32_t)xv[0] ^ kBias, (uint32_t)xv[1] ^ kBias, (uint32_t)xv[2] ^ kBias,
+                                (uint32_t)xv[3] ^ kBias};
+#pragma unroll
+        for (int nt = 0; nt < NTMAX; ++nt) {
+            if (nt < nt_live) {
+                v4i D[4];
+                D[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, Bw0[nt], Z, 0, 0, 0);
+                D[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, Bx[nt], Z, 0, 0, 0);
+                D[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, Bx[nt], C2[nt], 0, 0, 0);
+                D[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, Bw3[nt], Z, 0, 0, 0);
+                mf8_tile_epilogue<MASK>(D, sh[nt], xb, i0 + 4 * qq, st[nt], s32[nt]);
+            }
+        }
+    };
+    /* tiles T = wid, wid + nw, ...; the first two (samples < 32 >= every start) masked */
+    int T = wid;
+    while (T < 2 && T < ntile) {
+        tile(T, std::true_type{});
+        T += nw;
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTMAX; ++nt) acc[nt] += s32[nt], s32[nt] = 0;
+    while (T < ntile) {
+#pragma unroll 1
+        for (int g = 0; g < G && T < ntile; ++g, T += nw) tile(T, std::false_type{});
+#pragma unroll
+        for (int nt = 0; nt < NTMAX; ++nt) acc[nt] += s32[nt], s32[nt] = 0;
+    }
+#pragma unroll
+    for (int nt = 0; nt < NTMAX; ++nt) {
+        uint64_t v = acc[nt];
+        v += (uint64_t)__shfl_xor((unsigned long long)v, 16);
+        v += (uint64_t)__shfl_xor((unsigned long long)v, 32);
+        const int p = 16 * nt + col + 1;
+        if (lane < 16 && p <= LMAX) red[wid * NSUM + 4 + p] = p <= L ? v : 0ull;
+    }
+}
+
 /* Phase E of the fast kernel for a fixed predictor of order K (encoder.py:331-359,
  * common.py:15-21): the residual of samples i0..i0+7 is their K-th difference, zig-zagged
  * (utils.py:91-94); the warm-up samples i < K give 0.  16-bit samples: |r| < 2^19. */
@@ -680,6 +869,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     constexpr int HP = resid_hp(LMAX);
     constexpr int NSUM = 5 + LMAX;
     constexpr bool MF = S16 && (LMAX == 8 || LMAX == 12); /* MFMA candidate sums available */
+    constexpr bool MF8 = PATH == PATH_W64 && LMAX >= 16 && VAR != kVarFast; /* int8-MFMA sums available */
     static_assert(!FAST || (MF && sizeof(ResT) == 4), "FAST: S16 MFMA path with a 32-bit residual only");
 
     extern __shared__ __align__(16) unsigned char smem[];
@@ -700,7 +890,14 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
         if (n % (1 << o) == 0) rmax_eff = o;
     const bool regz = FAST || resid_regz(n, rmax_eff, !WIDE && sizeof(ResT) == 4);
     const ResidLds lay = resid_lds_layout(LMAX, n, nw, 1 << (rmax_eff < 0 ? 0 : rmax_eff), S16 ? 2 : 4,
-                                          (int)sizeof(ResT), CT::BYTES, regz, false);
+                                          (int)sizeof(ResT), CT::BYTES, regz, MF8);
+    /* int8-MFMA path: digit planes (alias the residual-side regions), |c| sums and the
+     * per-wave max|x| in the (unused) MFMA tap-table region */
+    const int PLB = mf8_plane_bytes(n);
+    int32_t* mf8_sabs = reinterpret_cast<int32_t*>(smem + lay.coef + CT::TAPF_OFF); /* [LMAX] */
+    uint32_t* mf8_xmax = reinterpret_cast<uint32_t*>(mf8_sabs + 64);               /* [nw] */
+    bool use_mf8 = false;
+    int mf8_G = 0;
     int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
     int32_t* xs32 = reinterpret_cast<int32_t*>(smem + lay.xs) + HP; /* [-HP, npad) (others) */
     ResT* zz = reinterpret_cast<ResT*>(smem + lay.zz);              /* [npad] (LDS-resident mode) */
@@ -846,8 +1043,50 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
         } else {
             const int32_t* __restrict__ src = (const int32_t*)a.samples + u * a.stride;
             const int nv = n >> 2;
-            for (int v = tid; v < nv; v += NT)
-                *reinterpret_cast<int4v*>(xs32 + 4 * v) = *reinterpret_cast<const int4v*>(src + 4 * v);
+            if (MF8 && a.mfma && do_lpc && L >= 1 && n % 16 == 0 && n >= 32) {
+                /* stage and split into the three digit planes in one pass; track max|x| and
+                 * whether every top digit fits a signed byte */
+                uint32_t* pw = reinterpret_cast<uint32_t*>(smem + lay.pl);
+                const int pwd = PLB >> 2;
+                uint32_t xm = 0;
+                bool b2ok = true;
+                for (int v = tid; v < nv; v += NT) {
+                    const int4v q = *reinterpret_cast<const int4v*>(src + 4 * v);
+                    *reinterpret_cast<int4v*>(xs32 + 4 * v) = q;
+                    uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        int32_t b0, b1, b2;
+                        mf8_digits(q[e], b0, b1, b2);
+                        b2ok &= b2 <= 127;
+                        const uint32_t ax = (uint32_t)(q[e] < 0 ? -q[e] : q[e]);
+                        xm = ax > xm ? ax : xm;
+                        w0 |= ((uint32_t)b0 & 255u) << (8 * e);
+                        w1 |= ((uint32_t)b1 & 255u) << (8 * e);
+                        w2 |= ((uint32_t)b2 & 255u) << (8 * e);
+                    }
+                    pw[(kMf8Pad >> 2) + v] = w0;
+                    pw[pwd + (kMf8Pad >> 2) + v] = w1;
+                    pw[2 * pwd + (kMf8Pad >> 2) + v] = w2;
+                }
+                /* zero pads: the first kMf8Pad bytes and the tail of each plane */
+                const int tail0 = (kMf8Pad + n) >> 2;
+                for (int i = tid; i < 3 * pwd; i += NT) {
+                    const int k = i % pwd;
+                    if (k < (kMf8Pad >> 2) || k >= tail0) pw[i] = 0u;
+                }
+                uint32_t wm = b2ok ? xm : 0xffffffffu;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const uint32_t t = (uint32_t)__shfl_xor((int)wm, o);
+                    wm = t > wm ? t : wm;
+                }
+                if (lane == 0) mf8_xmax[wid] = wm;
+            } else {
+                if (MF8 && tid < nw) mf8_xmax[tid] = 0xffffffffu;
+                for (int v = tid; v < nv; v += NT)
+                    *reinterpret_cast<int4v*>(xs32 + 4 * v) = *reinterpret_cast<const int4v*>(src + 4 * v);
+            }
             for (int i = nv * 4 + tid; i < n; i += NT) xs32[i] = src[i];
         }
     }
@@ -885,6 +1124,17 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 int sa = 1 << sh;
                 for (int j = 0; j <= i; ++j) sa += cp[j] < 0 ? -cp[j] : cp[j];
                 mf_ok &= sa <= kMfmaCoefLimit;
+            }
+            if (MF8) { /* sum|c| of order i+1, or -1 when a coefficient's top digit overflows */
+                int32_t sa = 0;
+                if (i < L) {
+                    const int32_t* cp = rec + 2 + L + (i * (i + 1)) / 2;
+                    for (int j = 0; j <= i; ++j) {
+                        const int32_t ac = cp[j] < 0 ? -cp[j] : cp[j];
+                        sa = (sa < 0 || cp[j] > 32639 || cp[j] < -32640) ? -1 : sa + ac;
+                    }
+                }
+                mf8_sabs[i] = sa;
             }
         }
     }
@@ -925,6 +1175,26 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
         __syncthreads();
     }
     }
+    if constexpr (MF8) {
+        if (a.sample_bytes == 4 && a.mfma && do_lpc && L >= 1 && n % 16 == 0 && n >= 32) {
+            /* the unit's bound B on |r| and |floor(pred / 2^s)| (uniform: LDS broadcasts) */
+            uint64_t xm = 0;
+            for (int w = 0; w < nw; ++w) xm = mf8_xmax[w] > xm ? mf8_xmax[w] : xm;
+            bool ok = xm < (1ull << 31);
+            uint64_t bmax = 0;
+            for (int i = 0; i < L && ok; ++i) {
+                const int32_t sa = mf8_sabs[i];
+                ok = sa >= 0;
+                const uint64_t b = xm + (((uint64_t)sa * xm) >> lsh[i]) + 1;
+                bmax = b > bmax ? b : bmax;
+            }
+            if (ok && bmax < (1ull << 29)) {
+                use_mf8 = true;
+                const uint64_t g = 0xffffffffull / (4 * bmax);
+                mf8_G = g > 64 ? 64 : (int)g;
+            }
+        }
+    }
     if (a.stop_after == 1) return;
 
     /* ---- phase B: sum|r| for fixed orders 0..4 and LPC orders 1..L ---- */
@@ -940,6 +1210,10 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
         if constexpr (MF)
             mfma_candidate_sums<LMAX>(xs16, reinterpret_cast<const float*>(smem + lay.coef + CT::TAPF_OFF), lsh, L,
                                       n, lane, wid, nw, red, sumx);
+        if (a.stop_after == 2) return;
+    } else if (MF8 && use_mf8) {
+        if constexpr (MF8)
+            mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid, nw, red);
         if (a.stop_after == 2) return;
     } else if constexpr (!FAST) {
     A acc[NSUM];
@@ -1471,7 +1745,7 @@ static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     const bool regz = resid_regz(a.n, rmax_eff, PATH != PATH_W64 && PATH != PATH_W64S && sizeof(ResT) == 4);
     const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, 1 << (rmax_eff < 0 ? 0 : rmax_eff),
                                         PATH == PATH_S16 ? 2 : 4, (int)sizeof(ResT), CoefTables<LMAX>::BYTES,
-                                        regz, false).total;
+                                        regz, PATH == PATH_W64 && LMAX >= 16).total;
     auto kern = k_resid<LMAX, PATH, ResT, kVarGeneric>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

@@ -269,6 +269,40 @@ def test_24bit_tones_narrow_and_wide_candidate_sums(az, q, noise):
     compare_with_oracle(out, ora, [n] * 16)
 
 
+@pytest.mark.parametrize("L", [16, 17, 24, 32])
+@pytest.mark.parametrize("bits", [20, 24])
+def test_int8_mfma_candidate_sums_orders(az, L, bits):
+    """PATH_W64 int8-MFMA candidate sums (k_resid.h mf8_*): both N-tiles, partial second
+    N-tile, masked warm-up tiles, 20/24-bit synthetic units and tones, against the oracle."""
+    n = 2048
+    a = oracle.synth_batch(0, 24, n, bits, 500 + L + bits, dtype=np.int32)
+    t = _tones24(8, n, L + bits, 2.0) >> (24 - bits)
+    a = np.concatenate([a, t])
+    for q in (15, 11):
+        out = az.analyze(a, make_params(L, q, 0, 6), n, sample_bits=bits, debug=True)
+        ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, 6), n, sample_bits=bits, threads=16)
+        compare_with_oracle(out, ora, [n] * len(a))
+
+
+def test_int8_mfma_fallbacks(az):
+    """Units the int8 path must hand to the int64 chains: a top digit of 128 (a sample above
+    8355711), n not a multiple of 16; next to ordinary units and the most negative sample."""
+    n = 2048
+    a = oracle.synth_batch(0, 12, n, 24, 77, dtype=np.int32)
+    a[1, 700] = 8355712
+    a[2, 5] = 2 ** 23 - 1
+    a[3, 1000:1100] = -2 ** 23
+    a[4, :] = a[4, :] // 2 + 8355711 // 2
+    out = az.analyze(a, make_params(32, 15, 0, 6), n, sample_bits=24, debug=True)
+    ora = oracle.analyze_batch(a, oracle.make_params(32, 15, 0, 6), n, sample_bits=24, threads=16)
+    compare_with_oracle(out, ora, [n] * len(a))
+    m = 2040  # n % 16 != 0
+    b = np.ascontiguousarray(a[:, :m])
+    out = az.analyze(b, make_params(32, 15, 0, 3), m, sample_bits=24, debug=True)
+    ora = oracle.analyze_batch(b, oracle.make_params(32, 15, 0, 3), m, sample_bits=24, threads=16)
+    compare_with_oracle(out, ora, [m] * len(b))
+
+
 def test_split_plane_path_opt_in():
     """PATH_W64S (opt-in, FLACMI_SPLIT=1, read once per process): config 3 shape and
     full-scale tones, in a child process, bit-exact against the oracle."""
