@@ -505,7 +505,8 @@ def main(argv=None):
                                   rank == 0 and not args.no_parity)
 
     e2e = None
-    if rank == 0 and world == 1 and args.e2e_units > 0 and not chunked:
+    # (FLACMI_DEBUG_STOP truncates k_resid: its metadata must never reach the frame writer)
+    if rank == 0 and world == 1 and args.e2e_units > 0 and not chunked and not os.environ.get("FLACMI_DEBUG_STOP"):
         e2e = end_to_end_leg(args, cfg, az)
 
     lpc_b, resid_b, pipe_b = algorithmic_bytes(cfg, meta_np, units)

@@ -528,17 +528,20 @@ __device__ __forceinline__ void mf8_digits(int32_t x, int32_t& b0, int32_t& b1, 
     b2 = (x1 - b1) >> 8;
 }
 
-/* 16 plane bytes from byte offset o (any alignment) */
-__device__ __forceinline__ v4i mf8_frag(const uint32_t* pw, int o) {
-    const int dw = o >> 2;
-    const uint32_t sh = (uint32_t)(o & 3);
-    const uint32_t d0 = pw[dw], d1 = pw[dw + 1], d2 = pw[dw + 2], d3 = pw[dw + 3], d4 = pw[dw + 4];
-    v4i r;
-    r[0] = (int)__builtin_amdgcn_alignbyte(d1, d0, sh);
-    r[1] = (int)__builtin_amdgcn_alignbyte(d2, d1, sh);
-    r[2] = (int)__builtin_amdgcn_alignbyte(d3, d2, sh);
-    r[3] = (int)__builtin_amdgcn_alignbyte(d4, d3, sh);
-    return r;
+/* a 16-byte window of a plane at any byte alignment: the five dwords that cover it (read
+ * one tile ahead), then four v_alignbyte by the window's byte offset within the first */
+struct Mf8Raw {
+    uint32_t d[5];
+};
+__device__ __forceinline__ void mf8_load(const uint32_t* pw, Mf8Raw& r) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) r.d[k] = pw[k];
+}
+__device__ __forceinline__ v4i mf8_align(const Mf8Raw& r, uint32_t sh) {
+    v4i v;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (int)__builtin_amdgcn_alignbyte(r.d[k + 1], r.d[k], sh);
+    return v;
 }
 
 /* one 16-sample tile for N-tile operands B*, accumulating |r| of the lane's column into s32 */
@@ -595,7 +598,6 @@ __device__ __forceinline__ void mf8_candidate_sums(const int32_t* xs32, const un
         }
     }
     const int col = lane & 15, qq = lane >> 4, sg = qq >> 1, h = qq & 1, m = col;
-    const int nt_live = L > 16 ? 2 : 1;
     /* B operands and per-column constants */
     v4i Bw0[NTMAX], Bx[NTMAX], Bw3[NTMAX], C2[NTMAX];
     int sh[NTMAX], st[NTMAX];
@@ -627,48 +629,108 @@ __device__ __forceinline__ void mf8_candidate_sums(const int32_t* xs32, const un
         const int cb = (int)(1u << (15 + sh[nt]));
         C2[nt] = v4i{cb, cb, cb, cb};
     }
+    /* the lane's three windows: plane 0; plane 1 (slot 0) or 0 (slot 1); plane 2 or 1.  A
+     * tile start is a multiple of 16 samples, so each window's byte alignment is fixed and
+     * tile T reads dwords 4T further on. */
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(pl);
     const int off0 = kMf8Pad + m - 16 - 16 * h;
     const int off1 = off0 + (sg == 0 ? PLB : 0);
     const int off2 = off0 + (sg == 0 ? 2 * PLB : PLB);
+    const uint32_t al = (uint32_t)(off0 & 3); /* PLB is a multiple of 16 */
+    const uint32_t* pw0 = pw + (off0 >> 2);
+    const uint32_t* pw1 = pw + (off1 >> 2);
+    const uint32_t* pw2 = pw + (off2 >> 2);
     const v4i Z{0, 0, 0, 0};
     uint64_t acc[NTMAX];
     uint32_t s32[NTMAX];
 #pragma unroll
     for (int nt = 0; nt < NTMAX; ++nt) acc[nt] = 0, s32[nt] = 0;
     const int ntile = n >> 4;
-    auto tile = [&](int T, auto MASK_) __attribute__((always_inline)) {
+    /* the MFMAs of one tile with NTL live N-tiles (windows from the raw dwords) */
+    auto mm = [&](const Mf8Raw& r0, const Mf8Raw& r1, const Mf8Raw& r2, auto& D) __attribute__((always_inline)) {
+        constexpr int NTL = sizeof(D) / sizeof(D[0]);
+        const v4i A0 = mf8_align(r0, al), A1 = mf8_align(r1, al), A2 = mf8_align(r2, al);
+#pragma unroll
+        for (int nt = 0; nt < NTL; ++nt) {
+            D[nt][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, Bw0[nt], Z, 0, 0, 0);
+            D[nt][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, Bx[nt], Z, 0, 0, 0);
+            D[nt][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, Bx[nt], C2[nt], 0, 0, 0);
+            D[nt][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, Bw3[nt], Z, 0, 0, 0);
+        }
+    };
+    /* |r| of tile T from its MFMA results */
+    auto ep = [&](const auto& D, int T, auto MASK_) __attribute__((always_inline)) {
+        constexpr int NTL = sizeof(D) / sizeof(D[0]);
         constexpr bool MASK = decltype(MASK_)::value;
         const int i0 = T << 4;
-        const v4i A0 = mf8_frag(pw, off0 + i0), A1 = mf8_frag(pw, off1 + i0), A2 = mf8_frag(pw, off2 + i0);
         const int4v xv = *reinterpret_cast<const int4v*>(xs32 + i0 + 4 * qq);
         const uint32_t xb[4] = {(uint32_t)xv[0] ^ kBias, (uint32_t)xv[1] ^ kBias, (uint32_t)xv[2] ^ kBias,
                                 (uint32_t)xv[3] ^ kBias};
 #pragma unroll
-        for (int nt = 0; nt < NTMAX; ++nt) {
-            if (nt < nt_live) {
-                v4i D[4];
-                D[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A0, Bw0[nt], Z, 0, 0, 0);
-                D[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A1, Bx[nt], Z, 0, 0, 0);
-                D[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, Bx[nt], C2[nt], 0, 0, 0);
-                D[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A2, Bw3[nt], Z, 0, 0, 0);
-                mf8_tile_epilogue<MASK>(D, sh[nt], xb, i0 + 4 * qq, st[nt], s32[nt]);
-            }
-        }
+        for (int nt = 0; nt < NTL; ++nt) mf8_tile_epilogue<MASK>(D[nt], sh[nt], xb, i0 + 4 * qq, st[nt], s32[nt]);
     };
-    /* tiles T = wid, wid + nw, ...; the first two (samples < 32 >= every start) masked */
-    int T = wid;
-    while (T < 2 && T < ntile) {
-        tile(T, std::true_type{});
-        T += nw;
-    }
-#pragma unroll
-    for (int nt = 0; nt < NTMAX; ++nt) acc[nt] += s32[nt], s32[nt] = 0;
-    while (T < ntile) {
-#pragma unroll 1
-        for (int g = 0; g < G && T < ntile; ++g, T += nw) tile(T, std::false_type{});
+    auto flush = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int nt = 0; nt < NTMAX; ++nt) acc[nt] += s32[nt], s32[nt] = 0;
+    };
+    /* tiles T = wid, wid + nw, ...; the first two (samples < 32 >= every start) masked.  The
+     * main loop is software-pipelined over two register sets: while the VALU runs the
+     * epilogue of tile T, the matrix cores run the MFMAs of the next tile and the LDS
+     * delivers the windows of the one after (clamped index: no guarded loads; a clamped
+     * tile's MFMAs are never used). */
+    auto run = [&](auto NTL_) __attribute__((always_inline)) {
+        constexpr int NTL = decltype(NTL_)::value;
+        int T = wid;
+        Mf8Raw a0, a1, a2, b0, b1, b2;
+        v4i DA[NTL][4], DB[NTL][4];
+        while (T < 2 && T < ntile) {
+            mf8_load(pw0 + 4 * T, a0);
+            mf8_load(pw1 + 4 * T, a1);
+            mf8_load(pw2 + 4 * T, a2);
+            mm(a0, a1, a2, DA);
+            ep(DA, T, std::true_type{});
+            T += nw;
+        }
+        flush();
+        if (T >= ntile) return;
+        mf8_load(pw0 + 4 * T, a0);
+        mf8_load(pw1 + 4 * T, a1);
+        mf8_load(pw2 + 4 * T, a2);
+        mm(a0, a1, a2, DA);
+        int Tn = T + nw < ntile ? T + nw : T;
+        mf8_load(pw0 + 4 * Tn, b0);
+        mf8_load(pw1 + 4 * Tn, b1);
+        mf8_load(pw2 + 4 * Tn, b2);
+        int g = 0;
+        for (;;) {
+            int Tnn = Tn + nw < ntile ? Tn + nw : Tn;
+            mm(b0, b1, b2, DB);
+            mf8_load(pw0 + 4 * Tnn, a0);
+            mf8_load(pw1 + 4 * Tnn, a1);
+            mf8_load(pw2 + 4 * Tnn, a2);
+            ep(DA, T, std::false_type{});
+            T += nw;
+            if (++g == G) flush(), g = 0;
+            if (T >= ntile) break;
+            Tn = Tnn;
+            Tnn = Tn + nw < ntile ? Tn + nw : Tn;
+            mm(a0, a1, a2, DA);
+            mf8_load(pw0 + 4 * Tnn, b0);
+            mf8_load(pw1 + 4 * Tnn, b1);
+            mf8_load(pw2 + 4 * Tnn, b2);
+            ep(DB, T, std::false_type{});
+            T += nw;
+            if (++g == G) flush(), g = 0;
+            if (T >= ntile) break;
+            Tn = Tnn;
+        }
+        flush();
+    };
+    if constexpr (NTMAX >= 2) {
+        if (L > 16) run(std::integral_constant<int, 2>{});
+        else run(std::integral_constant<int, 1>{});
+    } else {
+        run(std::integral_constant<int, 1>{});
     }
 #pragma unroll
     for (int nt = 0; nt < NTMAX; ++nt) {
@@ -894,8 +956,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     /* int8-MFMA path: digit planes (alias the residual-side regions), |c| sums and the
      * per-wave max|x| in the (unused) MFMA tap-table region */
     const int PLB = mf8_plane_bytes(n);
-    int32_t* mf8_sabs = reinterpret_cast<int32_t*>(smem + lay.coef + CT::TAPF_OFF); /* [LMAX] */
-    uint32_t* mf8_xmax = reinterpret_cast<uint32_t*>(mf8_sabs + 64);               /* [nw] */
+    uint32_t* mf8_xmax = reinterpret_cast<uint32_t*>(smem + lay.coef + CT::TAPF_OFF); /* [nw] */
     bool use_mf8 = false;
     int mf8_G = 0;
     int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
@@ -1050,24 +1111,38 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 const int pwd = PLB >> 2;
                 uint32_t xm = 0;
                 bool b2ok = true;
-                for (int v = tid; v < nv; v += NT) {
-                    const int4v q = *reinterpret_cast<const int4v*>(src + 4 * v);
-                    *reinterpret_cast<int4v*>(xs32 + 4 * v) = q;
-                    uint32_t w0 = 0, w1 = 0, w2 = 0;
+                /* eight 16-byte loads in flight per thread before any is used (clamped
+                 * indices, no guarded loads) */
+                constexpr int KB = 8;
+                for (int v0 = tid; v0 < nv; v0 += KB * NT) {
+                    int4v qv[KB];
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        int32_t b0, b1, b2;
-                        mf8_digits(q[e], b0, b1, b2);
-                        b2ok &= b2 <= 127;
-                        const uint32_t ax = (uint32_t)(q[e] < 0 ? -q[e] : q[e]);
-                        xm = ax > xm ? ax : xm;
-                        w0 |= ((uint32_t)b0 & 255u) << (8 * e);
-                        w1 |= ((uint32_t)b1 & 255u) << (8 * e);
-                        w2 |= ((uint32_t)b2 & 255u) << (8 * e);
+                    for (int k = 0; k < KB; ++k) {
+                        const int v = v0 + k * NT < nv ? v0 + k * NT : nv - 1;
+                        qv[k] = *reinterpret_cast<const int4v*>(src + 4 * v);
                     }
-                    pw[(kMf8Pad >> 2) + v] = w0;
-                    pw[pwd + (kMf8Pad >> 2) + v] = w1;
-                    pw[2 * pwd + (kMf8Pad >> 2) + v] = w2;
+#pragma unroll
+                    for (int k = 0; k < KB; ++k) {
+                        const int v = v0 + k * NT;
+                        if (v >= nv) break;
+                        const int4v q = qv[k];
+                        *reinterpret_cast<int4v*>(xs32 + 4 * v) = q;
+                        uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            int32_t b0, b1, b2;
+                            mf8_digits(q[e], b0, b1, b2);
+                            b2ok &= b2 <= 127;
+                            const uint32_t ax = (uint32_t)(q[e] < 0 ? -q[e] : q[e]);
+                            xm = ax > xm ? ax : xm;
+                            w0 |= ((uint32_t)b0 & 255u) << (8 * e);
+                            w1 |= ((uint32_t)b1 & 255u) << (8 * e);
+                            w2 |= ((uint32_t)b2 & 255u) << (8 * e);
+                        }
+                        pw[(kMf8Pad >> 2) + v] = w0;
+                        pw[pwd + (kMf8Pad >> 2) + v] = w1;
+                        pw[2 * pwd + (kMf8Pad >> 2) + v] = w2;
+                    }
                 }
                 /* zero pads: the first kMf8Pad bytes and the tail of each plane */
                 const int tail0 = (kMf8Pad + n) >> 2;
@@ -1125,17 +1200,6 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 for (int j = 0; j <= i; ++j) sa += cp[j] < 0 ? -cp[j] : cp[j];
                 mf_ok &= sa <= kMfmaCoefLimit;
             }
-            if (MF8) { /* sum|c| of order i+1, or -1 when a coefficient's top digit overflows */
-                int32_t sa = 0;
-                if (i < L) {
-                    const int32_t* cp = rec + 2 + L + (i * (i + 1)) / 2;
-                    for (int j = 0; j <= i; ++j) {
-                        const int32_t ac = cp[j] < 0 ? -cp[j] : cp[j];
-                        sa = (sa < 0 || cp[j] > 32639 || cp[j] < -32640) ? -1 : sa + ac;
-                    }
-                }
-                mf8_sabs[i] = sa;
-            }
         }
     }
     if constexpr (MF) {
@@ -1177,21 +1241,41 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     }
     if constexpr (MF8) {
         if (a.sample_bytes == 4 && a.mfma && do_lpc && L >= 1 && n % 16 == 0 && n >= 32) {
-            /* the unit's bound B on |r| and |floor(pred / 2^s)| (uniform: LDS broadcasts) */
-            uint64_t xm = 0;
-            for (int w = 0; w < nw; ++w) xm = mf8_xmax[w] > xm ? mf8_xmax[w] : xm;
-            bool ok = xm < (1ull << 31);
-            uint64_t bmax = 0;
-            for (int i = 0; i < L && ok; ++i) {
-                const int32_t sa = mf8_sabs[i];
-                ok = sa >= 0;
-                const uint64_t b = xm + (((uint64_t)sa * xm) >> lsh[i]) + 1;
-                bmax = b > bmax ? b : bmax;
+            /* the unit's bound B on |r| and |floor(pred / 2^s)|, lane-parallel over the
+             * orders (lane p-1) and reduced over the wave: every wave gets the same answer */
+            uint32_t xm = lane < nw ? mf8_xmax[lane] : 0u;
+            uint64_t b = 0;
+            if (lane < L) {
+                const int p = lane + 1;
+                uint32_t sa = 0;
+                bool cok = true;
+#pragma unroll
+                for (int j = 0; j < LMAX; ++j) {
+                    const int32_t c = j < p ? cfl[lane * CT::CPAD + j] : 0;
+                    cok &= c <= 32639 && c >= -32640; /* the top coefficient digit fits a byte */
+                    sa += (uint32_t)(c < 0 ? -c : c);
+                }
+                b = cok ? ((uint64_t)sa << 32) | (uint32_t)lsh[lane] : ~0ull;
             }
-            if (ok && bmax < (1ull << 29)) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const uint32_t t = (uint32_t)__shfl_xor((int)xm, o);
+                xm = t > xm ? t : xm;
+            }
+            uint64_t bl = 0;
+            if (lane < L)
+                bl = b == ~0ull || xm >= (1u << 31) ? ~0ull
+                                                    : (uint64_t)xm + (((b >> 32) * (uint64_t)xm) >> (b & 31)) + 1;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const uint64_t t = (uint64_t)__shfl_xor((unsigned long long)bl, o);
+                bl = t > bl ? t : bl;
+            }
+            const uint64_t bmax = bl;
+            if (__builtin_amdgcn_readfirstlane((int)(bmax >> 29)) == 0) {
                 use_mf8 = true;
-                const uint64_t g = 0xffffffffull / (4 * bmax);
-                mf8_G = g > 64 ? 64 : (int)g;
+                const uint64_t g = 0xffffffffull / (4 * bmax); /* >= 2 under bmax < 2^29 */
+                mf8_G = __builtin_amdgcn_readfirstlane(g > 64 ? 64 : (int)g); /* wave-uniform */
             }
         }
     }
