@@ -117,9 +117,22 @@ class Analyzer:
             o.lpc_records = out["lpc_records"].ctypes.data
         check(self.lib.flacmi_analyze_host(self.ctx, C.byref(b), C.byref(params), C.byref(o)),
               "flacmi_analyze_host")
-        if residual_bytes == 4 and np.any(out["meta"]["status"] == abi.STATUS_RESIDUAL_WIDE):
-            # a chosen residual needs more than 32 bits: redo the batch with 64-bit rows
-            return self.analyze(samples, params, block_len, tail_len, n_tail_units, sample_bits, 8, debug)
+        wide = np.flatnonzero(out["meta"]["status"] == abi.STATUS_RESIDUAL_WIDE) if residual_bytes == 4 else []
+        if len(wide):
+            # a chosen residual needs more than 32 bits: redo only those units with 64-bit
+            # rows and widen the batch's rows (the other units' results stand)
+            first_tail = n_units - n_tail_units
+            sub = self.analyze(np.ascontiguousarray(s[wide]), params, block_len, tail_len,
+                               int(np.count_nonzero(wide >= first_tail)), sample_bits, 8, debug)
+            w = max(out["residual"].shape[1], sub["residual"].shape[1])
+            res = np.zeros((n_units, w), dtype=np.uint64)
+            res[:, :out["residual"].shape[1]] = out["residual"]
+            res[wide] = 0
+            res[wide, :sub["residual"].shape[1]] = sub["residual"]
+            out["residual"] = res
+            for k, v in sub.items():
+                if k != "residual":
+                    out[k][wide] = v
         return out
 
     def analyze_device(self, samples_ptr: int, sample_bytes: int, sample_bits: int, unit_stride: int,

@@ -356,3 +356,23 @@ def test_long_blocks_are_declared_unsupported(az):
         with pytest.raises(FlacmiError) as ei:
             az.analyze(rows, params, n)
         assert f"({abi.E_UNSUPPORTED})" in str(ei.value) and "LDS" in str(ei.value)
+
+
+def test_wide_chosen_residual_redoes_only_those_units(az):
+    """32-bit samples where the chosen residual needs more than 32 bits (a near-full-scale block
+    with one opposite spike: order 1 wins with |r| ~ 2^32) next to ordinary units and a short
+    tail unit: the analyzer redoes only the wide units with 64-bit rows; every unit equals
+    the oracle."""
+    n, nu = 1024, 8
+    a = oracle.synth_batch(0, nu, n, 32, 9, dtype=np.int32)
+    r = np.random.default_rng(5)
+    for u in (1, 4, 7):
+        a[u, :] = (2 ** 31 - 1000) + r.integers(-100, 100, n)
+        a[u, 300 + u] = -2 ** 31
+    a[7, 700:] = 0  # the tail unit (700 samples)
+    p = make_params(8, 12, 0, 4)  # sample_bits + q <= 44
+    out = az.analyze(a, p, n, 700, 1, sample_bits=32, debug=True)
+    ora = oracle.analyze_batch(a, oracle.make_params(8, 12, 0, 4), n, 700, 1, sample_bits=32, threads=8)
+    assert out["residual"].dtype == np.uint64
+    assert int(np.max(ora["residual"][1])) >= 2 ** 32
+    compare_with_oracle(out, ora, [n] * (nu - 1) + [700])
