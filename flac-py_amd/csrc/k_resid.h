@@ -841,6 +841,101 @@ __device__ __forceinline__ void rice_params_wave0(const ResidArgs& a, uint64_t s
     }
 }
 
+/* rice_params_wave0 for P = 64 J finest partitions (J = 2 or 4): lane k holds the sums of
+ * finest partitions J k .. J k + J - 1 (fin = the heap's finest nodes, read before pk, which
+ * aliases them, is written).  Orders omax .. omax - log2 J are lane-local (J >> d nodes per
+ * lane), the coarser ones a butterfly over lanes as in rice_params_wave0.  Same outputs:
+ * pk[16 f + o] for every finest partition f, rb[o] header bits, misc[0] the first error
+ * (smallest order, then smallest partition: the reference's evaluation order), misc[1] its
+ * site, misc[4] the orders with a parameter > 14.  Sums < 2^53: the parameter is the
+ * reference's float floor(log2(S / len)) (rice_floor_log2). */
+template <int J>
+__device__ __forceinline__ void rice_params_wave0_multi(const ResidArgs& a, const unsigned long long* fin,
+                                                        const double* tl, unsigned long long* rb, int* misc,
+                                                        uint8_t* pk, int n, int order, int rmin, int omax,
+                                                        int lane) {
+    constexpr int LJ = J == 4 ? 2 : 1;
+    uint64_t v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = fin[J * lane + j];
+    int ekey = -1, esite = 0;
+    uint32_t m5 = 0;
+    auto param = [&](uint64_t S, int len, bool& zero, bool& neg) __attribute__((always_inline)) -> int {
+        zero = S == 0;
+        neg = false;
+        if (zero) return 0;
+        const int prm = rice_floor_log2((double)S / (double)len, tl, a.log2thr);
+        neg = prm < 0;
+        return prm;
+    };
+    /* lane-local orders: d = 0 .. LJ (J >> d nodes per lane, node K = (J >> d) lane + jj) */
+    static_for<LJ + 1>([&](auto D_) {
+        constexpr int d = D_;
+        constexpr int NJ = J >> d;
+        const int o = omax - d;
+        if (o >= rmin) {
+            if constexpr (d > 0) {
+#pragma unroll
+                for (int jj = 0; jj < NJ; ++jj) v[jj] = v[2 * jj] + v[2 * jj + 1];
+            }
+            uint32_t hb = 0;
+            int efirst = -1, ezero = 0;
+#pragma unroll
+            for (int jj = NJ - 1; jj >= 0; --jj) {
+                const int K = NJ * lane + jj;
+                const int len = (n >> o) - (K == 0 ? order : 0);
+                bool zero, neg;
+                const int prm = param(v[jj], len, zero, neg);
+#pragma unroll
+                for (int f = 0; f < (1 << d); ++f) pk[16 * (J * lane + (jj << d) + f) + o] = (uint8_t)prm;
+                if (zero || neg) efirst = jj, ezero = zero;
+                if (prm > 14) m5 |= 1u << o; /* made wave-uniform below */
+                hb += 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm);
+            }
+            const unsigned long long eb = __ballot(efirst >= 0);
+            if (eb) {
+                const int kl = __builtin_ctzll(eb);
+                ekey = (o << 16) | (NJ * kl + __shfl(efirst, kl));
+                esite = __shfl(ezero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
+            }
+            const uint32_t ht = wave_sum_u32(hb);
+            if (lane == 0) rb[o] = ht;
+        }
+    });
+    /* coarser orders: one node per 2^(d - LJ) lanes */
+    uint64_t t = v[0];
+    for (int o = omax - LJ - 1; o >= rmin; --o) {
+        const int d = omax - o - LJ; /* >= 1 */
+        t += (uint64_t)__shfl_xor((unsigned long long)t, 1 << (d - 1));
+        const int K = lane >> d;
+        const bool lead = (lane & ((1 << d) - 1)) == 0;
+        const int len = (n >> o) - (K == 0 ? order : 0);
+        bool zero, neg;
+        const int prm = param(t, len, zero, neg);
+#pragma unroll
+        for (int j = 0; j < J; ++j) pk[16 * (J * lane + j) + o] = (uint8_t)prm;
+        const unsigned long long eb = __ballot(lead && (zero || neg));
+        if (eb) {
+            const int kl = __builtin_ctzll(eb);
+            ekey = (o << 16) | (kl >> d);
+            esite = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
+        }
+        if (__ballot(lead && prm > 14)) m5 |= 1u << o;
+        const uint32_t hb = lead ? 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm) : 0u;
+        const uint32_t ht = wave_sum_u32(hb);
+        if (lane == 0) rb[o] = ht;
+    }
+    /* lane-local m5 bits: OR over the wave */
+    uint32_t mo = m5;
+#pragma unroll
+    for (int sft = 32; sft >= 1; sft >>= 1) mo |= (uint32_t)__shfl_xor((int)mo, sft);
+    if (lane == 0) {
+        misc[0] = ekey;
+        misc[1] = esite;
+        misc[4] = (int)mo;
+    }
+}
+
 /* data bits of one chunk for every candidate order (chunk sum < 2^30 for narrow values) */
 __device__ __forceinline__ void chunk_rice_bits(const uint32_t (&z)[8], uint4 pv, int ro, int oo,
                                                 uint32_t (&tb)[16]) {
@@ -986,8 +1081,13 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     if constexpr (FAST) {
         int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.cs);
         const int16_t* __restrict__ src = (const int16_t*)a.samples + u * a.stride;
-        int32_t rw = 0;
-        if (tid < a.rec_words) rw = rec[tid];
+        /* the record (<= 92 words at L <= 12) in two loads per thread: a 64-thread
+         * workgroup (n <= 2560) needs both */
+        static_assert(LMAX <= 12, "FAST stages at most 2 * 64 record words");
+        int32_t rw[2] = {0, 0};
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (tid + j * NT < a.rec_words) rw[j] = rec[tid + j * NT];
         for (int i = tid; i < HP; i += NT) xs16[i - HP] = 0;
         for (int i = n + tid; i < resid_xpad(n); i += NT) xs16[i] = 0;
         for (int v = tid; v < (n >> 3); v += NT) { /* n % 8 == 0 */
@@ -1000,7 +1100,9 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 sumx += (uint32_t)(x0 < 0 ? -x0 : x0) + (uint32_t)(x1 < 0 ? -x1 : x1);
             }
         }
-        if (tid < a.rec_words) recl[tid] = rw;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (tid + j * NT < a.rec_words) recl[tid + j * NT] = rw[j];
         if (tid == 0) {
             misc[0] = 0x7fffffff;
             misc[1] = 0;
@@ -1055,13 +1157,9 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
         use_mfma = __syncthreads_and(mf_ok) && a.mfma;
     } else {
 
-    if (ref_mode) {
-        const int st = rec[0];
-        if (st != 0) { /* the reference raises inside encode_subframe_lpc */
-            if (tid == 0) put_meta(meta, st & 0xffff, st >> 16, nullptr, 0);
-            return;
-        }
-    }
+    /* the unit's LPC status: loaded now, tested after the staging loads are in flight (a
+     * test here would put one more HBM round trip in front of them) */
+    const int st_rec = ref_mode ? rec[0] : 0;
     if constexpr (S16) {
         for (int i = tid; i < HP; i += NT) xs16[i - HP] = 0;
         for (int i = n + tid; i < resid_xpad(n); i += NT) xs16[i] = 0;
@@ -1165,13 +1263,19 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             for (int i = nv * 4 + tid; i < n; i += NT) xs32[i] = src[i];
         }
     }
+    if (st_rec != 0) { /* the reference raises inside encode_subframe_lpc */
+        if (tid == 0) put_meta(meta, st_rec & 0xffff, st_rec >> 16, nullptr, 0);
+        return;
+    }
     if (do_lpc) {
         const uint32_t negmask = (uint32_t)rec[1];
         for (int i = tid; i < LMAX * CT::CPAD; i += NT) {
             const int pp = i / CT::CPAD + 1, j = i % CT::CPAD;
             cfl[i] = (pp <= L && j < pp) ? rec[2 + L + (pp * (pp - 1)) / 2 + j] : 0;
         }
-        /* pair t of order pp: (lo = c[2t], hi = c[2t-1]) with c[-1] = -2^shift (S16 path) */
+        /* pair t of order pp: (lo = c[2t], hi = c[2t-1]) with c[-1] = -2^shift (S16 and
+         * W64S paths only) */
+        if (S16 || SPLIT)
         for (int i = tid; i < LMAX * CT::PPAD; i += NT) {
             const int pp = i / CT::PPAD + 1, t = i % CT::PPAD;
             const int32_t* cp = rec + 2 + L + (pp * (pp - 1)) / 2;
@@ -1613,11 +1717,30 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
         }
     }
     if constexpr (!FAST) {
+    /* WIDE, 32-bit rows, 64..256 finest partitions of at most 64 whole chunks each: the
+     * finest partition sums are reduced here across the cpp consecutive lanes that own a
+     * partition's chunks, into the heap's finest nodes, for rice_params_wave0(_multi) */
+    int wr_om = -1, wr_cpp = 0;
+    if constexpr (WIDE && sizeof(ResT) == 4) {
+        const int om = first_order();
+        if (om >= 6 && om <= 8 && ((n >> om) & 7) == 0 && (n >> om) >> 3 <= 64 && a.mode != FLACMI_MODE_LPC_ONLY) {
+            wr_om = om;
+            wr_cpp = (n >> om) >> 3;
+        }
+    }
+    wr_om = __builtin_amdgcn_readfirstlane(wr_om);
 #pragma unroll 1
     for (int c = tid; c < nch; c += NT) {
         ResT zv[8];
         resid_chunk(c, zv);
         store_chunk(c, zv);
+        if (WIDE && sizeof(ResT) == 4 && wr_om >= 0) {
+            uint64_t cs8 = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) cs8 += (uint64_t)zv[k];
+            for (int w = 1; w < wr_cpp; w <<= 1) cs8 += (uint64_t)__shfl_xor((unsigned long long)cs8, w);
+            if ((c & (wr_cpp - 1)) == 0) hs[(1 << wr_om) + c / wr_cpp] = cs8;
+        }
         if constexpr (sizeof(ResT) == 4) {
             reinterpret_cast<uint4*>(zz + 8 * c)[0] = uint4{zv[0], zv[1], zv[2], zv[3]};
             reinterpret_cast<uint4*>(zz + 8 * c)[1] = uint4{zv[4], zv[5], zv[6], zv[7]};
@@ -1677,6 +1800,84 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 chunk_rice_bits(z, *reinterpret_cast<const uint4*>(pk + 16 * (c / cpp)), ro, oo, tb);
             }
             rice_finish(a, meta, dec, tb, rb, red, misc, pk, n, start, rmin, omax, tid, NT, lane, wid, nw, gid);
+            return;
+        }
+    }
+    if constexpr (WIDE && sizeof(ResT) == 4) {
+        if (wr_om >= 0) {
+            /* wave 0: every order's parameters from the finest sums phase E left in hs[P..2P)
+             * (no heap pyramid, no barriers between orders, no contended atomics) */
+            uint8_t* pk = reinterpret_cast<uint8_t*>(hs);
+            if (wid == 0) {
+                if (P == 64) rice_params_wave0<false>(a, hs[P + lane], tl, rb, misc, pk, n, order, rmin, omax, lane);
+                else if (P == 128) rice_params_wave0_multi<2>(a, hs + P, tl, rb, misc, pk, n, order, rmin, omax, lane);
+                else rice_params_wave0_multi<4>(a, hs + P, tl, rb, misc, pk, n, order, rmin, omax, lane);
+            }
+            __syncthreads();
+            if (misc[0] >= 0) {
+                if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
+                return;
+            }
+            const int cpp = ps >> 3;
+            const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+            const uint4* pkv = reinterpret_cast<const uint4*>(hs);
+            uint64_t tb[16];
+#pragma unroll
+            for (int o = 0; o < 16; ++o) tb[o] = 0;
+            for (int c = tid; c < nch; c += NT) {
+                const uint4 u = reinterpret_cast<const uint4*>(zz)[2 * c], v = reinterpret_cast<const uint4*>(zz)[2 * c + 1];
+                const uint32_t z[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                const uint4 pv = pkv[c / cpp];
+                if (((u.x | u.y | u.z | u.w | v.x | v.y | v.z | v.w) >> 29) == 0) {
+                    uint32_t t32[16];
+#pragma unroll
+                    for (int o = 0; o < 16; ++o) t32[o] = 0;
+                    chunk_rice_bits(z, pv, ro, oo, t32);
+#pragma unroll
+                    for (int o = 0; o < 16; ++o)
+                        if (o >= ro && o <= oo) tb[o] += t32[o];
+                } else {
+                    const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+                    for (int o = 0; o < 16; ++o)
+                        if (o >= ro && o <= oo) {
+                            const uint32_t p = (pw[o >> 2] >> (8 * (o & 3))) & 0xffu;
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) tb[o] += (uint64_t)(z[k] >> p);
+                        }
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < 16; ++o)
+                if (o >= ro && o <= oo) {
+                    const uint64_t w = wave_sum_u64(tb[o]);
+                    if (lane == 0) red[wid * 16 + o] = w;
+                }
+            __syncthreads();
+            if (tid == 0) {
+                int best = -1;
+                unsigned long long bb = 0;
+                for (int o = rmin; o <= omax; ++o) {
+                    unsigned long long v = rb[o];
+                    for (int w2 = 0; w2 < nw; ++w2) v += red[w2 * 16 + o];
+                    if (best < 0 || v < bb) {
+                        bb = v;
+                        best = o;
+                    }
+                }
+                put_meta(meta, ST_OK, 0, dec, 1);
+                meta->res_offset = start;
+                meta->res_len = n - start;
+                meta->part_order = best;
+                meta->n_parts = 1 << best;
+                meta->coding_method = ((misc[4] >> best) & 1) ? 5 : 4;
+                meta->rice_bits = (long long)bb;
+                misc[3] = best;
+            }
+            __syncthreads();
+            const int best = misc[3];
+            int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
+            for (int K = tid; K < (1 << best); K += NT) rp[K] = pk[16 * (K << (omax - best)) + best];
             return;
         }
     }

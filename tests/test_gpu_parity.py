@@ -376,3 +376,35 @@ def test_wide_chosen_residual_redoes_only_those_units(az):
     assert out["residual"].dtype == np.uint64
     assert int(np.max(ora["residual"][1])) >= 2 ** 32
     compare_with_oracle(out, ora, [n] * (nu - 1) + [700])
+
+
+@pytest.mark.parametrize("n,rmax", [(4096, 8), (2048, 6), (8192, 7)])
+def test_wide_rice_wave0_parameters_and_errors(az, n, rmax):
+    """PATH_W64 with 64..256 finest partitions: wave 0 derives every order's parameters from
+    the finest sums phase E reduced (rice_params_wave0 / _multi).  Silent stretches give a zero
+    partition sum (log of 0: ValueError), sparse +-1 stretches a mean below 1 (negative
+    parameter); loud units exercise Rice5Bit parameters (> 14) at every level."""
+    r = np.random.default_rng(n + rmax)
+    a = oracle.synth_batch(0, 16, n, 24, n + rmax, dtype=np.int32)
+    a[1, n // 2:] = 0                                    # zero partitions (coarse orders still fine)
+    a[2, :] = 0
+    a[2, ::97] = r.integers(-1, 2, len(a[2, ::97]))      # sums below the partition length
+    a[3, 3 * n // 4:] = 0
+    a[3, 3 * n // 4::5] = 1
+    a[4, :] = r.integers(-2 ** 23, 2 ** 23, n)           # white full-scale noise: parameters > 14
+    a[5, : n // 8] = 0                                   # silent start (first partition shorter)
+    a[6, :] = (r.integers(-3, 4, n) * (np.arange(n) % 512 < 64)).astype(np.int32)
+    out = az.analyze(a, make_params(32, 15, 0, rmax), n, sample_bits=24, debug=True)
+    ora = oracle.analyze_batch(a, oracle.make_params(32, 15, 0, rmax), n, sample_bits=24, threads=16)
+    sts = set(int(v) for v in ora["meta"]["status"])
+    compare_with_oracle(out, ora, [n] * len(a))
+    assert len(sts) >= 2, sts
+
+
+@pytest.mark.parametrize("rmin,rmax", [(0, 6), (3, 2)])
+def test_fast_kernel_stages_the_whole_record(az, rmin, rmax):
+    """The S16 fast kernel with a 64-thread workgroup (n = 1024) and L = 12: the LPC record
+    (92 words) is longer than the workgroup, so each thread stages two words.  Many units per
+    launch, so a word left unstaged would read another unit's record from LDS.  r 0..6 and
+    the empty Rice range keep k_resid_stream out (more than 32 finest partitions / none)."""
+    batch_case(az, 256, 1024, 16, 31 + rmin, 12, 5, rmin, rmax)
