@@ -1600,8 +1600,16 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 }
                 r = (int64_t)(w[HP + k] - (pred >> dshift));
             } else {
+                /* only the chosen predictor's taps: coefficients past its order are zero
+                 * (a fixed predictor, the common choice, has at most 4) */
                 int64_t pred = 0;
-                static_for<TAPS>([&](auto J_) { pred += (int64_t)cf[J_] * (int64_t)w[HP + k - 1 - J_]; });
+                auto taps = [&](auto NT_) __attribute__((always_inline)) {
+                    static_for<decltype(NT_)::value>(
+                        [&](auto J_) { pred += (int64_t)cf[J_] * (int64_t)w[HP + k - 1 - J_]; });
+                };
+                if (order <= 4) taps(std::integral_constant<int, (TAPS < 4 ? TAPS : 4)>{});
+                else if (sizeof(ResT) == 4 && order <= 16) taps(std::integral_constant<int, (TAPS < 16 ? TAPS : 16)>{});
+                else taps(std::integral_constant<int, TAPS>{});
                 r = (int64_t)w[HP + k] - (pred >> dshift);
             }
             const int i = i0 + k;
