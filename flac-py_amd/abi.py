@@ -211,6 +211,8 @@ SIGNATURES = {
     "flacmi_encode_pipeline": (C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Params), C.POINTER(FrameParams),
                                          C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                          C.POINTER(EncodeTiming)]),
+    "flacmi_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "flacmi_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
     "flacmi_decode_frames_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                               C.POINTER(DecodeParams), C.POINTER(Batch), C.c_void_p, C.c_int64,
                                               C.c_void_p, C.c_void_p, C.c_void_p]),

@@ -196,11 +196,13 @@ class Analyzer:
 
     def encode_pipeline(self, samples: np.ndarray, params: abi.Params, block_len: int, tail_len: int = 0,
                         n_tail_units: int = 0, sample_bits: int = 16, channels: int = 1, sample_size: int = 16,
-                        first_frame: int = 0, units_per_batch: int = 8192, capacity: int = 0):
+                        first_frame: int = 0, units_per_batch: int = 8192, capacity: int = 0,
+                        out: np.ndarray = None):
         """encode_frames through flacmi_encode_pipeline: host rows in (any row stride), the
         batch streamed through the device in sub-batches of units_per_batch units with the
-        PCIe copies overlapping the kernels.  Returns (frame bytes, frame offsets
-        [n_frames + 1], frame status [n_frames], timing dict)."""
+        PCIe copies overlapping the kernels.  `out` (optional, uint8): the caller's frame
+        buffer, reused across calls (with host_register it stays page-locked).  Returns
+        (frame bytes, frame offsets [n_frames + 1], frame status [n_frames], timing dict)."""
         s = samples
         if s.dtype not in (np.int16, np.int32) or s.ndim != 2 or s.strides[1] != s.itemsize:
             raise ValueError("samples must be a 2-D int16 or int32 array with contiguous rows")
@@ -221,9 +223,14 @@ class Analyzer:
         offsets = np.zeros(n_frames + 1, dtype=np.int64)
         status = np.zeros(max(n_frames, 1), dtype=np.int32)
         upb = max(channels, (units_per_batch // channels) * channels)
+        if out is not None:
+            if out.dtype != np.uint8 or out.ndim != 1 or not out.flags.c_contiguous:
+                raise ValueError("out must be a contiguous 1-D uint8 array")
+            capacity = out.size
         cap = capacity or int(n_units * (block_len * s.itemsize * 1.25 + 256)) + (1 << 20)
+        given = out
         while True:
-            out = np.empty(cap, dtype=np.uint8)
+            out = given if given is not None else np.empty(cap, dtype=np.uint8)
             t = abi.EncodeTiming()
             rc = self.lib.flacmi_encode_pipeline(self.ctx, C.byref(b), C.byref(params), C.byref(fp), upb,
                                                  out.ctypes.data, cap, offsets.ctypes.data, status.ctypes.data,
@@ -235,6 +242,13 @@ class Analyzer:
             break
         timing = {f: getattr(t, f) for f, _ in abi.EncodeTiming._fields_}
         return out[:int(offsets[-1])], offsets, status[:n_frames], timing
+
+    def host_register(self, a: np.ndarray) -> None:
+        """Page-lock a host array until host_unregister (flacmi_host_register)."""
+        check(self.lib.flacmi_host_register(self.ctx, a.ctypes.data, a.nbytes), "flacmi_host_register")
+
+    def host_unregister(self, a: np.ndarray) -> None:
+        check(self.lib.flacmi_host_unregister(self.ctx, a.ctypes.data), "flacmi_host_unregister")
 
     def frame_sizes_device(self, batch: abi.Batch, fp: abi.FrameParams, meta_ptr: int, params_ptr: int,
                            params_stride: int, offsets_ptr: int, status_ptr: int, stream: int = 0) -> None:

@@ -921,6 +921,20 @@ static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, co
     return 0;
 }
 
+extern "C" int flacmi_host_register(flacmi_ctx* ctx, void* ptr, size_t bytes) {
+    if (!ctx || !ptr || bytes == 0) return fail(FLACMI_E_INVALID, "null context, pointer or empty range");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return 0;
+}
+
+extern "C" int flacmi_host_unregister(flacmi_ctx* ctx, void* ptr) {
+    if (!ctx || !ptr) return fail(FLACMI_E_INVALID, "null context or pointer");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipHostUnregister(ptr));
+    return 0;
+}
+
 extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_params* params,
                                       const flacmi_frame_params* fp, int64_t units_per_batch, uint8_t* out,
                                       int64_t out_capacity, int64_t* frame_offsets, int32_t* frame_status,
@@ -944,8 +958,17 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
     /* the caller's rows and output, page-locked in place for the call */
     const auto r0 = std::chrono::steady_clock::now();
     const size_t in_bytes = (size_t)((batch->n_units - 1) * batch->unit_stride + batch->block_len) * batch->sample_bytes;
-    const bool reg_in = hipHostRegister(const_cast<void*>(batch->samples), in_bytes, hipHostRegisterDefault) == hipSuccess;
-    const bool reg_out = out_capacity > 0 && hipHostRegister(out, (size_t)out_capacity, hipHostRegisterDefault) == hipSuccess;
+    /* a buffer already page-locked (flacmi_host_register, hipHostMalloc) is used as it is */
+    auto locked = [](const void* q) {
+        hipPointerAttribute_t at{};
+        const bool y = hipPointerGetAttributes(&at, q) == hipSuccess && at.type == hipMemoryTypeHost;
+        (void)hipGetLastError();
+        return y;
+    };
+    const bool reg_in = !locked(batch->samples) &&
+                        hipHostRegister(const_cast<void*>(batch->samples), in_bytes, hipHostRegisterDefault) == hipSuccess;
+    const bool reg_out = out_capacity > 0 && !locked(out) &&
+                         hipHostRegister(out, (size_t)out_capacity, hipHostRegisterDefault) == hipSuccess;
     (void)hipGetLastError();
     t.register_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
     constexpr int kEncSlots = 3;

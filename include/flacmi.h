@@ -244,6 +244,9 @@ int flacmi_encode_fetch(flacmi_ctx* ctx, uint8_t* out, int64_t bytes);
  * flight: the copy of sub-batch k+1 to the device and its analysis overlap the frame
  * writing and the copy back of sub-batch k.  The caller's sample rows and `out` are
  * page-locked in place for the call (hipHostRegister) so both copies are DMA at PCIe rate.
+ * Buffers the caller already page-locked with flacmi_host_register are used as they are
+ * (no per-call register / unregister: the way to stream many calls through the same
+ * buffers).
  * out receives the frames back to back; frame_offsets[n_frames + 1] their byte offsets and
  * frame_status[n_frames] as flacmi_frame_sizes_device (a failing frame has no bytes).
  * FLACMI_E_NOMEM if the frames exceed out_capacity (frame_offsets then hold the sizes of
@@ -264,6 +267,15 @@ int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch, const fla
                            const flacmi_frame_params* fp, int64_t units_per_batch, uint8_t* out,
                            int64_t out_capacity, int64_t* frame_offsets, int32_t* frame_status,
                            flacmi_encode_timing* timing);
+
+/* Page-lock a host range for the lifetime the caller chooses (hipHostRegister on the
+ * context's device), so repeated flacmi_encode_pipeline / flacmi_analyze_host calls over
+ * the same buffers copy at PCIe rate without paying the page-locking each call.  Replaces
+ * nothing in the reference (its encode() has no device copies); the host-side analogue of
+ * keeping a reused buffer (__main__.py:94-109 writes one output file per run).
+ * FLACMI_E_HIP if the range cannot be locked (e.g. it overlaps a locked range). */
+int flacmi_host_register(flacmi_ctx* ctx, void* ptr, size_t bytes);
+int flacmi_host_unregister(flacmi_ctx* ctx, void* ptr);
 
 /* ---- decoder verifier (BASELINE config 5 round trip) ------------- */
 /* Replaces the reference's frame decoder: decoder.py:111-130 get_frame, :133-190

@@ -156,3 +156,29 @@ def test_encode_pipeline_equals_encode_frames(az, name, upb):
     assert data.tobytes() == want[0].tobytes(), name
     assert timing["sub_batches"] == (frames + upb - 1) // upb
     assert timing["bytes_out"] == int(offsets[-1])
+
+
+def test_encode_pipeline_with_caller_pinned_buffers(az):
+    """Rows and frame buffer page-locked once by the caller (flacmi_host_register): the
+    pipeline uses them as they are (no per-call locking) and two calls through the same
+    buffers give the one-shot path's bytes."""
+    frames, C, n, tail, bits, L, q, rmin, rmax, mode, ss, first, seed = CASES["c2"]
+    rows, n_tail = _rows(frames, C, n, tail, bits, seed)
+    params = oracle.make_params(L, q, rmin, rmax, mode)
+    want = az.encode_frames(rows, params, n, tail, n_tail, sample_bits=bits, channels=C, sample_size=ss,
+                            first_frame=first)
+    rows = np.ascontiguousarray(rows)
+    out = np.zeros(len(want[0]) + 4096, dtype=np.uint8)
+    az.host_register(rows)
+    az.host_register(out)
+    try:
+        for _ in range(2):
+            data, offsets, status, t = az.encode_pipeline(rows, params, n, tail, n_tail, sample_bits=bits,
+                                                          channels=C, sample_size=ss, first_frame=first,
+                                                          units_per_batch=5 * C, out=out)
+            assert np.array_equal(offsets, want[1]) and np.array_equal(status, want[2])
+            assert data.tobytes() == want[0].tobytes()
+            assert t["register_ms"] < 50.0
+    finally:
+        az.host_unregister(out)
+        az.host_unregister(rows)

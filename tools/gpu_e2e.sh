@@ -1,0 +1,9 @@
+# frames/pipeline GPU tests, then the default bench line (end-to-end leg included)
+set -o pipefail
+OUT=gpurun_out/${1:-e2e}
+mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_frames.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc $(tail -1 $OUT/pytest.log)"
+[ $rc -eq 0 ] || { grep -E "^E |FAILED" $OUT/pytest.log | head; exit 1; }
+timeout -k 10 400 python bench.py --cpu-seconds 2 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$OUT/bench.json'));e=d['end_to_end'];print(d['value'], json.dumps(e)[:900])"
