@@ -564,6 +564,8 @@ def main(argv=None):
                        "mode": "fixed-only" if cfg["mode"] else "reference", "parallelism": f"dp{world} (block shards)"},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": dom_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dom_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": (os.path.relpath(tfile, REPO) + ": rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
+                                            "of this config (tools/profile.sh, tools/traffic.py)") if traffic else None,
                          "algorithmic_bytes_per_launch": dom_bytes},
             "kernels": {"k_lpc_ms": kt["lpc_ms"], "k_resid_ms": kt["resid_ms"], "call_ms": kt["call_ms"],
                         "k_lpc_GBs": lpc_gbs, "k_resid_GBs": resid_gbs,
