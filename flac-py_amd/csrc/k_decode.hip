@@ -301,6 +301,12 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
         }
         if (g.pos > end_bit) { fail(DS_EOF); break; }
         const int esc_code = (1 << pbits) - 1;
+        /* FIXED subframes (the encoder's usual choice) predict from the last four samples held
+         * in registers, not from the LDS ring; LPC subframes read the ring */
+        const bool fx = t >= 8 && t <= 12;
+        const int32_t fc0 = fx ? fixed_coef(order, 0) : 0, fc1 = fx ? fixed_coef(order, 1) : 0,
+                      fc2 = fx ? fixed_coef(order, 2) : 0, fc3 = fx ? fixed_coef(order, 3) : 0;
+        int32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0; /* samples i-1 .. i-4 */
         int rem = plen - order, param = 0, escw = -1;
         bool first = true, eof = false;
         int32_t* orow = a.out ? a.out + u * a.out_stride : nullptr;
@@ -327,10 +333,18 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
                 const int64_t r = escw >= 0 ? g.sint(escw) : g.rice(param, end_bit, eof);
                 if (eof) { fail(DS_EOF); break; }
                 int64_t acc = 0;
-                for (int j = 0; j < order; ++j) acc += (int64_t)coef[j][lane] * ring[(i - 1 - j) & 31][lane];
+                if (fx) {
+                    acc = (int64_t)fc0 * h0 + (int64_t)fc1 * h1 + (int64_t)fc2 * h2 + (int64_t)fc3 * h3;
+                } else {
+                    for (int j = 0; j < order; ++j) acc += (int64_t)coef[j][lane] * ring[(i - 1 - j) & 31][lane];
+                }
                 s = r + (acc >> shift);
             }
             ring[i & 31][lane] = (int32_t)s;
+            h3 = h2;
+            h2 = h1;
+            h1 = h0;
+            h0 = (int32_t)s;
             if ((i & 31) == 31 || i == bs - 1) { /* flush the ring column */
                 const int c0 = i & ~31, cnt = i - c0 + 1;
                 if (orow) {
