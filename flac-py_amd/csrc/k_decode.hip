@@ -85,7 +85,16 @@ struct BitReader {
     int64_t pos; /* absolute bit position */
     int64_t bw;
     uint64_t buf;
+    /* CRC-16 of the frame folded as whole dwords leave the window, in stream order: dword
+     * cnext is the next one due, dwords below cend are inside the CRC range (crc16_fused) */
+    const uint16_t* ct = nullptr;
+    uint32_t crc = 0;
+    int64_t cnext = 0, cend = 0;
     __device__ __forceinline__ uint32_t ld(int64_t i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
+    __device__ __forceinline__ void fold(uint32_t be) { /* one whole big-endian dword */
+        const uint32_t v = be ^ (crc << 16);
+        crc = ct[3 * 256 + (v >> 24)] ^ ct[2 * 256 + ((v >> 16) & 0xFF)] ^ ct[256 + ((v >> 8) & 0xFF)] ^ ct[v & 0xFF];
+    }
     __device__ __forceinline__ void seek(int64_t p) {
         pos = p;
         bw = p >> 5;
@@ -96,6 +105,10 @@ struct BitReader {
         int64_t off = pos - (bw << 5);
         if (off > 32) {
             if (off < 64) {
+                if (ct && bw == cnext && bw < cend) { /* dword bw leaves the window */
+                    fold((uint32_t)(buf >> 32));
+                    ++cnext;
+                }
                 buf = (buf << 32) | ld(bw + 2);
                 bw += 1;
                 off -= 32;
@@ -159,6 +172,20 @@ __device__ __forceinline__ int32_t expect_at(const DecodeArgs& a, int64_t u, int
     return ((const int32_t*)a.expect)[u * a.expect_stride + i];
 }
 
+/* CRC-16 (crc.py:25-31) of stream bytes [b0, b1), continuing from c: slice-by-4 over
+ * whole dwords */
+__device__ uint32_t crc16_more(const DecodeArgs& a, const uint16_t* t, uint32_t c, int64_t b0, int64_t b1) {
+    const uint8_t* bytes = reinterpret_cast<const uint8_t*>(a.words);
+    int64_t i = b0;
+    for (; i < b1 && (i & 3); ++i) c = ((c << 8) & 0xFFFF) ^ t[((c >> 8) ^ bytes[i]) & 0xFF];
+    for (; i + 4 <= b1; i += 4) {
+        const uint32_t v = __builtin_bswap32(a.words[i >> 2]) ^ (c << 16);
+        c = t[3 * 256 + (v >> 24)] ^ t[2 * 256 + ((v >> 16) & 0xFF)] ^ t[256 + ((v >> 8) & 0xFF)] ^ t[v & 0xFF];
+    }
+    for (; i < b1; ++i) c = ((c << 8) & 0xFFFF) ^ t[((c >> 8) ^ bytes[i]) & 0xFF];
+    return c;
+}
+
 /* CRC-16 (crc.py:25-31) of stream bytes [b0, b1): slice-by-4 over whole dwords */
 __device__ uint32_t crc16_range(const DecodeArgs& a, const uint16_t* t, int64_t b0, int64_t b1) {
     const uint8_t* bytes = reinterpret_cast<const uint8_t*>(a.words);
@@ -194,6 +221,16 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
     BitReader g;
     g.w = a.words;
     g.nw = a.n_words;
+    /* fused CRC-16 over [F, Fend - 2): the bytes before the first whole dword now, whole
+     * dwords as they leave the window, the rest after the footer */
+    const int64_t E = Fend - 2;
+    const int64_t Fh = (F + 3) & ~(int64_t)3;
+    if (a.check_crc && E > F) {
+        g.ct = crct;
+        g.crc = crc16_more(a, crct, 0u, F, E < Fh ? E : Fh);
+        g.cnext = Fh >> 2;
+        g.cend = E >> 2;
+    }
     g.seek(F * 8);
     /* a parse failure after the reader ran off the stream is the EOFError of that read */
     auto pfail = [&](int32_t site) { fail(g.pos > end_bit ? (int32_t)DS_EOF : site); };
@@ -399,7 +436,18 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
         if (g.pos > end_bit) fail(DS_EOF);
         else {
             if ((g.pos >> 3) != Fend) fail(DS_FRAME_END);
-            if (a.check_crc && crc16_range(a, crct, F, (g.pos >> 3) - 2) != crc16) fail(DS_CRC16);
+            if (a.check_crc) {
+                uint32_t c;
+                if ((g.pos >> 3) == Fend && E > F) { /* the fused CRC: dwords not yet folded, then the tail */
+                    c = g.crc;
+                    const int64_t d0 = g.cnext, d1 = g.cend;
+                    if (d1 > d0) c = crc16_more(a, crct, c, 4 * d0, 4 * d1);
+                    if (4 * d1 >= Fh) c = crc16_more(a, crct, c, 4 * d1 > Fh ? 4 * d1 : Fh, E);
+                } else {
+                    c = crc16_range(a, crct, F, (g.pos >> 3) - 2);
+                }
+                if (c != crc16) fail(DS_CRC16);
+            }
         }
     }
     if (!is_ref_error(st) && neg_shift) fail(DS_NEG_SHIFT);

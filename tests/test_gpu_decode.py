@@ -117,3 +117,22 @@ def test_corruption_is_caught(az):
     # without the CRC / number checks the clean stream is accepted as the reference would
     _, st3, _ = az.decode_frames(data, offsets, C, ss, first_frame=-1, block_len=n, check_crc=False)
     assert not st3.any()
+
+
+def test_crc16_fused_in_the_bit_reader(az):
+    """k_decode folds each frame's CRC-16 as whole dwords leave its bit window (head and tail
+    bytes apart).  Flipping a bit of the stored CRC-16 of frames at every byte alignment
+    flags exactly those frames (crc16); the clean stream passes."""
+    rows, data, offsets, (C, n, tail, n_tail, ss, first) = _encode(az, "c2")
+    nf = len(offsets) - 1
+    picks = []
+    for al in range(4):  # up to four frames starting at each byte alignment
+        picks += [f for f in range(nf) if int(offsets[f]) % 4 == al][:4]
+    assert {int(offsets[f]) % 4 for f in picks} == {0, 1, 2, 3}
+    bad = data.copy()
+    for k, f in enumerate(picks):
+        bad[int(offsets[f + 1]) - 1 - (k & 1)] ^= 0x01 << (k % 8)
+    _, st, mm = az.decode_frames(bad, offsets, C, ss, first_frame=first, expect=rows, block_len=n)
+    assert sorted(i for i, s in enumerate(st) if s) == sorted(picks)
+    assert all((int(st[f]) >> 16) == abi.DSITE["crc16"] for f in picks)
+    assert not mm.any()
