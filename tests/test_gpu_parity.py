@@ -408,3 +408,48 @@ def test_fast_kernel_stages_the_whole_record(az, rmin, rmax):
     launch, so a word left unstaged would read another unit's record from LDS.  r 0..6 and
     the empty Rice range keep k_resid_stream out (more than 32 finest partitions / none)."""
     batch_case(az, 256, 1024, 16, 31 + rmin, 12, 5, rmin, rmax)
+
+
+def _meta_params_residual_equal(a, b, u):
+    am, bm = a["meta"], b["meta"]
+    for f in abi.META_DTYPE.names:
+        if f == "reserved0":
+            continue
+        assert np.array_equal(am[f][u], bm[f][u]), (u, f, am[f][u], bm[f][u])
+    if int(am["status"][u]) == 0:
+        k = int(am["n_parts"][u])
+        assert np.array_equal(a["rice_params"][u][:k], b["rice_params"][u][:k]), (u, "params")
+        off, ln = int(am["res_offset"][u]), int(am["res_len"][u])
+        assert np.array_equal(a["residual"][u][off:off + ln], b["residual"][u][off:off + ln]), (u, "residual")
+
+
+@pytest.mark.parametrize("entry", list(_golden_cases()))
+def test_golden_without_debug_outputs(az, entry):
+    """The production call (no debug outputs) against the debug run that
+    test_device_matches_reference_golden pins to the reference: every golden unit, fixed/LPC
+    winner, tie assertion and exception included, gives the same meta, parameters and
+    residual."""
+    xs = G.samples_for(entry, oracle.synth_unit)
+    bits = entry["params"]["sample_size"] if entry["source"]["kind"] == "synth" else 16
+    bits = max(bits, max((abs(v) for v in xs), default=0).bit_length() + 1)
+    p = make_params(**G.params_of(entry))
+    full = run_units(az, [xs], len(xs), p, bits=bits, debug=True)
+    pruned = run_units(az, [xs], len(xs), p, bits=bits, debug=False)
+    _meta_params_residual_equal(pruned, full, 0)
+
+
+@pytest.mark.parametrize("q", [5, 7, 9])
+def test_production_call_near_tied_orders_vs_oracle(az, q):
+    """Config-2 shape batches through the production call (no debug outputs) against the
+    oracle, plus units whose LPC orders nearly tie: pure tones (several orders predict them
+    equally well) and quantisation-limited noise."""
+    n = 4608
+    a = oracle.synth_batch(0, 160, n, 16, 900 + q, dtype=np.int16)
+    t = np.arange(n)
+    for u in range(8):
+        a[u] = np.round(8000 * np.sin(2 * np.pi * (u + 1) * 37.0 / 4608 * t)).astype(np.int16)
+    r = np.random.default_rng(q)
+    a[8:16] = r.integers(-3, 4, (8, n)).astype(np.int16)
+    out = az.analyze(a, make_params(12, q, 0, 5), n, sample_bits=16, debug=False)
+    ora = oracle.analyze_batch(a, oracle.make_params(12, q, 0, 5), n, sample_bits=16, threads=16)
+    compare_with_oracle(out, ora, [n] * len(a))
