@@ -87,6 +87,61 @@ __global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
         if constexpr (PK == 2) return (t & 1) ? (int32_t)v[t >> 1] >> 16 : (int32_t)(v[t >> 1] << 16) >> 16;
         return (int32_t)v[t];
     };
+    if constexpr (PK == 1) {
+        /* 32-bit samples (L up to 32, S = 40): loading whole S-sample blocks would hold 2 x 40
+         * sample registers beside the 33 accumulators and the 40-slot ring (one wave per SIMD,
+         * accumulators spilled to AGPRs).  Instead groups of G samples are prefetched one group
+         * ahead while the ring cycles through its S slots (static indices throughout). */
+        constexpr int G = 8;
+        static_assert(S % G == 0, "ring length a multiple of the load group");
+        const int ncyc = (M + S - 1) / S;
+        uint32_t gc[G], gn[G];
+        auto loadg = [&](int m0, uint32_t (&v)[G]) __attribute__((always_inline)) {
+            if (m0 + G <= M) {
+                const uint4 q0 = *reinterpret_cast<const uint4*>(x + m0);
+                const uint4 q1 = *reinterpret_cast<const uint4*>(x + m0 + 4);
+                v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w;
+                v[4] = q1.x; v[5] = q1.y; v[6] = q1.z; v[7] = q1.w;
+            } else {
+#pragma unroll
+                for (int k = 0; k < G; ++k) v[k] = (m0 + k < M) ? (uint32_t)x[m0 + k] : 0u;
+            }
+        };
+        if (ncyc > 0) loadg(0, gc);
+        for (int c = 0; c < ncyc; ++c) {
+            const int m0 = c * S;
+            const bool rect = m0 - LMAX >= a.fuse_lo && m0 + S <= a.fuse_hi;
+#pragma unroll
+            for (int g = 0; g < S / G; ++g) {
+                const int mg = m0 + g * G;
+                loadg(mg + G, gn);
+                if (rect) { /* exact integer products: one fused op per term (see below) */
+#pragma unroll
+                    for (int k = 0; k < G; ++k) {
+                        const int t = g * G + k;
+                        const double av = (double)(int32_t)gc[k];
+                        ring[t] = av;
+#pragma unroll
+                        for (int l = 0; l <= LMAX; ++l) acc[l] = __builtin_fma(ring[(t - l + S) % S], av, acc[l]);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < G; ++k) {
+                        const int t = g * G + k;
+                        const double av = (double)(int32_t)gc[k] * win[mg + k];
+                        ring[t] = av;
+#pragma unroll
+                        for (int l = 0; l <= LMAX; ++l) {
+                            const double prev = ring[(t - l + S) % S];
+                            acc[l] = acc[l] + prev * av;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < G; ++k) gc[k] = gn[k];
+            }
+        }
+    } else {
     if (nblk > 0) load(0, cur);
     for (int b = 0; b < nblk; ++b) {
         const int mb = b * SB;
@@ -124,6 +179,7 @@ __global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
 #pragma unroll
         for (int w = 0; w < W; ++w) cur[w] = nxt[w];
     }
+    } /* PK == 2 */
     if (a.acf) {
         double* o = a.acf + gid * 33;
 #pragma unroll
