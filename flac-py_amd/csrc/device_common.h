@@ -197,7 +197,11 @@ __host__ __device__ inline int resid_xpad(int n) {
  * balanced base-256 digits, sample i at byte kMf8Pad + i of its plane, zero outside
  * [0, n); the 16-byte tail keeps every 5-dword fragment read inside the plane. */
 constexpr int kMf8Pad = 32;
-__host__ __device__ inline int mf8_plane_bytes(int n) { return ((n + kMf8Pad + 16) + 15) & ~15; }
+__host__ __device__ inline int mf8_plane_bytes(int n) {
+    /* planes 128 B (32 banks) apart modulo 256 B: the slot-1 lanes' windows (another plane)
+     * fall on the other half of the banks from the slot-0 lanes' */
+    return ((n + kMf8Pad + 16 + 255) & ~255) + 128;
+}
 
 struct ResidLds {
     int xs, pl, zz, cs, coef, red, dec, rb, misc, hs, hp, tl, total;
