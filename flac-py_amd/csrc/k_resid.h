@@ -1242,11 +1242,12 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                         pw[2 * pwd + (kMf8Pad >> 2) + v] = w2;
                     }
                 }
-                /* zero pads: the first kMf8Pad bytes and the tail of each plane */
-                const int tail0 = (kMf8Pad + n) >> 2;
-                for (int i = tid; i < 3 * pwd; i += NT) {
-                    const int k = i % pwd;
-                    if (k < (kMf8Pad >> 2) || k >= tail0) pw[i] = 0u;
+                /* zero pads: the first kMf8Pad bytes and the tail of each plane (only those
+                 * dwords: npad of them per plane) */
+                const int tail0 = (kMf8Pad + n) >> 2, head = kMf8Pad >> 2, npad = head + (pwd - tail0);
+                for (int i = tid; i < 3 * npad; i += NT) {
+                    const int pl = i / npad, k = i - pl * npad;
+                    pw[pl * pwd + (k < head ? k : tail0 + (k - head))] = 0u;
                 }
                 uint32_t wm = b2ok ? xm : 0xffffffffu;
 #pragma unroll
