@@ -370,6 +370,29 @@ def shard_plan(cfg, rank, world, units, total_units_arg=0):
     return 0, list(range(rank, n_chunks, world)), total
 
 
+def run_chunks(az, cfg, params, bufs, chunk_ids, units, total_units, seed, stream=0, on_chunk=None):
+    """One rank's share of a chunked job (config 4): for each of its round-robin chunks,
+    generate the chunk's blocks on the device (global block index = chunk * units + i, the
+    frame number of the reference's block loop, encoder.py:87-97), analyse them and add the
+    chunk's stream statistics into bufs["stats_acc"] (zeroed first).  on_chunk(ci, cu), if
+    given, runs after each chunk's analysis (tests sample the chunk's units there)."""
+    n, bits = cfg["n"], cfg["bits"]
+    samples, meta, rparams, residual = bufs["samples"], bufs["meta"], bufs["rparams"], bufs["residual"]
+    sbytes = samples.element_size()
+    sstride, pstride, rstride = samples.shape[1], rparams.shape[1], residual.shape[1]
+    bufs["stats_acc"].zero_()
+    for ci in chunk_ids:
+        cu = min(units, total_units - ci * units)
+        az.synth_device(samples.data_ptr(), sbytes, bits, sstride, ci * units, cu, n, seed, stream)
+        az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, cu, n, params, meta.data_ptr(),
+                          rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, stream)
+        az.stream_stats(meta.data_ptr(), cu, n, bufs["stats"].data_ptr(), stream)
+        bufs["stats_acc"].add_(bufs["stats"])
+        if on_chunk is not None:
+            on_chunk(ci, cu)
+    return bufs["stats_acc"]
+
+
 def launch_check(args, cfg, units):
     """Multi-rank plumbing without a GPU (gloo): each rank reports its shard as a stats
     vector [units, samples, first, last+1, rank bit]; the all-reduced vector must cover
@@ -452,6 +475,7 @@ def main(argv=None):
     params = make_params(cfg["L"], cfg["q"], cfg["rmin"], cfg["rmax"], cfg["mode"])
 
     stats_acc = torch.zeros_like(stats)
+    bufs = dict(samples=samples, meta=meta, rparams=rparams, residual=residual, stats=stats, stats_acc=stats_acc)
 
     def step():
         if not chunked:
@@ -460,14 +484,7 @@ def main(argv=None):
             az.stream_stats(meta.data_ptr(), units, n, stats.data_ptr(), sptr)
             reduce_stats(stats, dist)
             return
-        stats_acc.zero_()
-        for ci in my_chunks:  # round-robin chunks: generate, analyse, count
-            cu = min(units, total_units - ci * units)
-            az.synth_device(samples.data_ptr(), sbytes, bits, sstride, ci * units, cu, n, args.seed, sptr)
-            az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, cu, n, params, meta.data_ptr(),
-                              rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, sptr)
-            az.stream_stats(meta.data_ptr(), cu, n, stats.data_ptr(), sptr)
-            stats_acc.add_(stats)
+        run_chunks(az, cfg, params, bufs, my_chunks, units, total_units, args.seed, sptr)
         reduce_stats(stats_acc, dist)
         stats.copy_(stats_acc)
 
@@ -506,18 +523,19 @@ def main(argv=None):
                                    cfg["rmax"], cfg["mode"]), n, sample_bits=bits, threads=16)
         res_host = residual[torch.as_tensor(pick, device=dev)].cpu().numpy().view(np.uint32)
         par_host = rparams[torch.as_tensor(pick, device=dev)].cpu().numpy()
-        bad = 0
+        bad = pruned = 0
         for j, u in enumerate(pick):
             g, o = meta_np[u], ora["meta"][j]
-            same = all(g[f] == o[f] for f in abi.META_DTYPE.names if f != "coefs") and \
-                np.array_equal(g["coefs"], o["coefs"])
+            same = not oracle.meta_mismatches(g, o)
+            pruned += int(g["lpc_order"]) == abi.LPC_PRUNED
             off, ln = int(o["res_offset"]), int(o["res_len"])
             same = same and np.array_equal(res_host[j][off:off + ln].astype(np.uint64), ora["residual"][j][off:off + ln])
             k = int(o["n_parts"])
             same = same and np.array_equal(par_host[j][:k], ora["rice_params"][j][:k])
             bad += 0 if same else 1
-        parity = {"units_checked": int(len(pick)), "mismatches": bad,
-                  "check": "meta, coefficients, zig-zag residual and Rice parameters bit-exact vs oracle"}
+        parity = {"units_checked": int(len(pick)), "mismatches": bad, "lpc_pruned": pruned,
+                  "check": "meta, coefficients, zig-zag residual and Rice parameters bit-exact vs oracle "
+                           "(a unit reporting FLACMI_LPC_PRUNED must lose to fixed in the oracle too)"}
 
     frames = None
     if not args.no_frames and not chunked:
@@ -544,7 +562,8 @@ def main(argv=None):
             traffic = None
 
     if rank == 0:
-        cpu = cpu_baseline(cfg, args.cpu_seconds, args.seed) if (world == 1 and args.cpu_seconds > 0) else None
+        # rank 0 only, after the timed region (the other ranks are idle by then)
+        cpu = cpu_baseline(cfg, args.cpu_seconds, args.seed) if args.cpu_seconds > 0 else None
         line = {
             "metric": METRIC,
             "value": value,
@@ -576,7 +595,8 @@ def main(argv=None):
             "end_to_end": e2e,
             "parity": parity,
             "stream_stats": {"units": int(st[0]), "samples": int(st[1]), "rice_bits": int(st[2]),
-                             "fixed": int(st[3]), "lpc": int(st[4]), "errors": int(st[65:80].sum())},
+                             "fixed": int(st[3]), "lpc": int(st[4]), "lpc_pruned": int(st[81]),
+                             "errors": int(st[65:80].sum())},
         }
         print(json.dumps(line), flush=True)
     az.close()

@@ -405,6 +405,16 @@ static int use_stream() {
     return v;
 }
 
+/* FLACMI_NO_PRUNE=1 computes every LPC candidate's exact sum in reference mode, as
+ * FLACMI_FLAG_ALL_CANDIDATES does per call (comparison runs). */
+static int prune_allowed() {
+    static const int v = [] {
+        const char* e = getenv("FLACMI_NO_PRUNE");
+        return (e && atoi(e) != 0) ? 0 : 1;
+    }();
+    return v;
+}
+
 /* FLACMI_OVERLAP=k (k > 1): k_lpc and k_resid of consecutive chunks overlap on two
  * streams (see analyze_device_impl); chunks hold at least kOverlapMinUnits units. */
 constexpr int64_t kOverlapMinUnits = 16384;
@@ -512,6 +522,8 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.retry_list = (int64_t*)ctx->retry.p + 2;
         a.sample_bits = b->sample_bits;
         a.stream = use_stream();
+        a.prune = p->mode == FLACMI_MODE_REFERENCE && !o->lpc_sums && !(p->reserved[1] & FLACMI_FLAG_ALL_CANDIDATES) &&
+                  prune_allowed();
         const bool wide = needs_wide(k.n, b->sample_bits, L, p->qlp_precision, p->mode);
         int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
         if (path == 2 && o->residual_bytes == 4 && split_ok(b->sample_bits, L, p->qlp_precision)) path = 3;

@@ -52,6 +52,9 @@ struct ResidArgs {
     int64_t* retry_list;             /* and their batch indices (NULL: no fast path) */
     int32_t sample_bits;             /* declared sample width (bounds the 64-bit paths' narrow sums) */
     int32_t stream;                  /* 1 = k_resid_stream where the shape allows (env FLACMI_NO_STREAM=1 -> 0) */
+    int32_t prune;                   /* 1 = reference mode may skip the exact LPC candidate sums of a unit
+                                        whose lower bounds already lose to the best fixed sum
+                                        (meta lpc_order = lpc_sum = FLACMI_LPC_PRUNED) */
 };
 /* internal unit status between the fast and the generic k_resid (never returned) */
 #define FLACMI_STATUS_RETRY 0x7e
@@ -118,6 +121,8 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes);
 constexpr int kMaxFinestParts = 4096;
 
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);
+/* test knob: fill every CU's LDS with a pattern (env FLACMI_POISON_LDS), else nothing */
+hipError_t launch_poison_lds(hipStream_t s);
 /* k_lpc<32> with the autocorrelation read from a.acf (flacmi_device_lpc_from_acf) */
 hipError_t launch_lpc_from_acf(const LpcArgs& a, hipStream_t s);
 /* path: 0 = int16 samples / sdot2, 1 = int32 samples / mad24, 2 = int64 arithmetic */

@@ -10,6 +10,7 @@ hipError_t launch_resid_l12(const ResidArgs&, int, int, hipStream_t);
 hipError_t launch_resid_l16(const ResidArgs&, int, int, hipStream_t);
 hipError_t launch_resid_l32(const ResidArgs&, int, int, hipStream_t);
 bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes);
+hipError_t launch_poison_lds(hipStream_t s);
 hipError_t launch_resid_stream(const ResidArgs& a, hipStream_t s);
 
 /* ====================================================================================
@@ -115,13 +116,51 @@ __global__ __launch_bounds__(256) void k_stats(const flacmi_unit_meta* __restric
             atomicAdd(&h[9 + (m.order >= 1 && m.order <= 32 ? m.order : 32)], 1ull);
         }
         atomicAdd(&h[48 + (m.part_order & 15)], 1ull);
+        if (m.lpc_order == FLACMI_LPC_PRUNED) atomicAdd(&h[81], 1ull);
+        /* reference-visible results only (lpc_sum may be FLACMI_LPC_PRUNED) */
         unsigned long long hsh = (unsigned long long)m.rice_bits * 0x9E3779B97F4A7C15ull ^
-                                 ((unsigned long long)m.fixed_sum << 1) ^ (unsigned long long)m.lpc_sum;
+                                 ((unsigned long long)m.fixed_sum << 1) ^
+                                 (unsigned long long)(m.kind * 64 + m.order) * 0xD1B54A32D192ED03ull;
         atomicAdd(&h[80], hsh);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < FLACMI_STATS_WORDS; i += blockDim.x)
         if (h[i]) atomicAdd(&stats[i], h[i]);
+}
+
+/* ---- LDS poisoning (test knob FLACMI_POISON_LDS=<hex pattern>, read once per process) ----
+ * Before every analysis kernel launch, one 160 KB workgroup per CU slot fills the LDS with a
+ * pattern derived from <pattern>, so a kernel that reads LDS words it never wrote sees
+ * garbage (and its results change with the pattern) instead of a previous unit's words.
+ * Off unless the variable is set. */
+__global__ __launch_bounds__(1024) void k_poison_lds(uint32_t pattern, int32_t words) {
+    extern __shared__ uint32_t lds_words[];
+    for (int i = threadIdx.x; i < words; i += blockDim.x)
+        lds_words[i] = pattern ^ ((uint32_t)i * 0x9E3779B1u) ^ (blockIdx.x << 20);
+    __syncthreads();
+    /* keep the stores: one lane publishes a word nobody reads if the pattern says so */
+    if (pattern == 0x5a5a5a5au && threadIdx.x == 0 && blockIdx.x == 0xffffff) lds_words[0] = lds_words[words - 1];
+}
+
+static uint32_t poison_pattern(bool* on) {
+    static const uint64_t v = [] {
+        const char* e = getenv("FLACMI_POISON_LDS");
+        return e ? (1ull << 32) | (uint64_t)(uint32_t)strtoul(e, nullptr, 16) : 0ull;
+    }();
+    *on = (v >> 32) != 0;
+    return (uint32_t)v;
+}
+
+hipError_t launch_poison_lds(hipStream_t s) {
+    bool on = false;
+    const uint32_t pat = poison_pattern(&on);
+    if (!on) return hipSuccess;
+    static uint32_t calls = 0;
+    const int bytes = 160 * 1024;
+    hipError_t e = hipFuncSetAttribute((const void*)k_poison_lds, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_poison_lds, dim3(1024), dim3(1024), bytes, s, pat ^ (++calls * 0x01000193u), bytes / 4);
+    return hipGetLastError();
 }
 
 static int lmax_bucket(int L) { return L <= 0 ? 0 : L <= 8 ? 8 : L <= 12 ? 12 : L <= 16 ? 16 : 32; }
@@ -136,6 +175,7 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes) {
 
 hipError_t launch_resid(const ResidArgs& a, int path, int residual_bytes, hipStream_t s) {
     if (a.count <= 0) return hipSuccess;
+    if (hipError_t e = launch_poison_lds(s); e != hipSuccess) return e;
     if (stream_shape_ok(a, path, residual_bytes)) return launch_resid_stream(a, s);
     const int lb = (a.mode == FLACMI_MODE_FIXED_ONLY || a.mode == FLACMI_MODE_RICE_ONLY) ? 0 : lmax_bucket(a.L);
     switch (lb) {

@@ -2056,7 +2056,8 @@ static hipError_t launch_resid_fast(const ResidArgs& a, hipStream_t s) {
     const int nt = resid_threads(a.n);
     const int P = 1 << (rmax_eff < 0 ? 0 : rmax_eff);
     const size_t lds_fast = resid_lds_layout(LMAX, a.n, nt / 64, P, 2, 4, CoefTables<LMAX>::BYTES, true, false).total;
-    const size_t lds_gen = resid_lds_layout(LMAX, a.n, nt / 64, P, 2, 4, CoefTables<LMAX>::BYTES, true, false).total;
+    const size_t lds_gen = resid_lds_layout(LMAX, a.n, nt / 64, P, 2, 4, CoefTables<LMAX>::BYTES,
+                                            resid_regz(a.n, rmax_eff, true), false).total;
     hipError_t e = hipMemsetAsync(a.retry_count, 0, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
     auto kf = k_resid<LMAX, PATH_S16, uint32_t, kVarFast>;
@@ -2064,6 +2065,7 @@ static hipError_t launch_resid_fast(const ResidArgs& a, hipStream_t s) {
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kf, dim3((unsigned)a.count), dim3(nt), lds_fast, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_poison_lds(s)) != hipSuccess) return e;
     /* the listed units: one workgroup each; the rest of the grid exits on the count */
     auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
     e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gen);
@@ -2080,7 +2082,10 @@ static hipError_t launch_resid_list(const ResidArgs& a, hipStream_t s) {
         if (a.n % (1 << o) == 0) rmax_eff = o;
     const int nt = resid_threads(a.n);
     const int P = 1 << (rmax_eff < 0 ? 0 : rmax_eff);
-    const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, P, 2, 4, CoefTables<LMAX>::BYTES, true, false).total;
+    /* the list variant carves its LDS with resid_regz (k_stream takes n up to 8*kSCPT*256,
+     * beyond the register-resident bound 8*kCPT*256): size it the same way */
+    const bool regz = resid_regz(a.n, rmax_eff, true);
+    const size_t lds = resid_lds_layout(LMAX, a.n, nt / 64, P, 2, 4, CoefTables<LMAX>::BYTES, regz, false).total;
     auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
     hipError_t e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

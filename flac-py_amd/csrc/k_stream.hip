@@ -4,7 +4,7 @@
  * Same results as k_resid (k_resid.h) bit for bit; it replaces k_resid's launch where the
  * shape allows (host check: stream_shape_ok):
  *   int16 samples, 32-bit residual rows, reference mode with 1 <= L <= 12 or fixed-only
- *   mode, n % 64 == 0, 64 <= n <= 6144, at most 32 finest Rice partitions of whole
+ *   mode, n % 64 == 0, 64 <= n <= 8 * kSCPT * 256 (10240), at most 32 finest Rice partitions of whole
  *   8-sample chunks.
  *
  * Reference semantics (flac/encoder.py): fixed predictors 331-359, LPC candidate residuals
@@ -70,7 +70,7 @@ struct SLds {
  *   xs   biased samples behind a 16-sample zero pad             staging .. Rice recompute
  *   pk   u16 [P][order] Rice parameters                         Rice (after B3)
  *   rec  the unit's LPC record (aliases pk)                     staging .. choice (before B3)
- *   red  u32 [nw][group][order][kb pair] MFMA partial sums      MFMA phase .. choice
+ *   red  u64 [nw][group][order] MFMA partial sums               MFMA phase .. choice
  *   red2 u64 [nw + 1][order] data bits (aliases red)            Rice (after B3)
  *   red0 u32 [nw] sum|x|                                         staging .. choice
  *   pks  u32 [P] finest partition sums                          staging (zeroed) .. Rice */
@@ -81,7 +81,7 @@ __host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P) 
     int o = 0;
     l.xs = o;   o = up(o + 2 * (kSHP + n));
     l.pk = l.rec = o; o = up(o + mx(2 * P * kRiceOrders, 4 * mx(rec_words, 1)));
-    l.red = l.red2 = o; o = up(o + mx(4 * nw * 32, 8 * (nw + 1) * kRiceOrders));
+    l.red = l.red2 = o; o = up(o + mx(8 * nw * 16, 8 * (nw + 1) * kRiceOrders));
     l.red0 = o; o = up(o + 4 * nw);
     l.pks = o;  o = up(o + 4 * P);
     l.total = o;
@@ -283,7 +283,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     const SLds lay = stream_lds(n, nw, rw, Pmax);
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem + lay.xs) + kSHP;
     int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.rec);
-    uint32_t* red = reinterpret_cast<uint32_t*>(smem + lay.red);
     uint32_t* red0 = reinterpret_cast<uint32_t*>(smem + lay.red0);
     unsigned long long* red2 = reinterpret_cast<unsigned long long*>(smem + lay.red2);
     uint32_t* pks = reinterpret_cast<uint32_t*>(smem + lay.pks); /* finest partition sums */
@@ -372,7 +371,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     }
     if (a.stop_after == 1) return;
 
-    /* ---- candidate sums on MFMA ---- */
+    /* ---- candidate sums on MFMA ----
+     * Exact mode: every block runs all NG + 1 groups and the LPC values are exact
+     * (floor(T / 2^shift), one shift + one sad each).
+     * Pruning mode (a.prune): every block runs the fixed group (exact: the fixed choice needs
+     * exact sums); every other block of a wave also runs the LPC groups, but accumulates the
+     * bound |T| (one sad).  For any subset S of a candidate's values
+     *   sum_all |r| >= sum_S |r| >= sum_S (|T| / 2^s - 1) >= sum_lanes floor(acc / 2^s) - n,
+     * since |floor(T / 2^s)| >= |T| / 2^s - (1 - 2^-s).  When that bound exceeds the best fixed
+     * sum for every order, LPC loses strictly (encoder.py:135-157: no win, no tie) and its
+     * exact sums are never needed.  Otherwise the LPC groups run again, exact, over every
+     * block (a workgroup-uniform branch: every wave decides from the same LDS words). */
+    const bool prune = NG > 0 && a.prune;
+    unsigned long long* red64 = reinterpret_cast<unsigned long long*>(smem + lay.red); /* [nw][4 groups][4 orders] */
+    auto lane_total = [&]() __attribute__((always_inline)) -> uint64_t {
+        /* lanes 1..4: fixed orders 1..4, lane 0: order 0 (sum|x|), lanes 16..15+4NG: LPC orders */
+        uint64_t t = 0;
+        int g = -1, o4l = 0;
+        if (lane >= 1 && lane <= 4) {
+            g = 0;
+            o4l = lane - 1;
+        } else if (NG > 0 && lane >= 16 && lane < 16 + 4 * NG) {
+            g = 1 + ((lane - 16) >> 2);
+            o4l = (lane - 16) & 3;
+        }
+        if (g >= 0) {
+#pragma unroll 1
+            for (int w2 = 0; w2 < nw; ++w2) t += red64[(w2 * 4 + g) * 4 + o4l];
+        } else if (lane == 0) {
+#pragma unroll 1
+            for (int w2 = 0; w2 < nw; ++w2) t += red0[w2];
+        }
+        return t;
+    };
+    uint64_t tj = 0;
+    bool pruned = false;
     {
         const int col = lane & 15, kb = lane >> 4, o4 = col >> 2, rho = col & 3;
         h8 B[NG + 1];
@@ -419,81 +452,110 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         uint32_t acc[NG + 1];
 #pragma unroll
         for (int g = 0; g <= NG; ++g) acc[g] = 0;
-        auto block = [&](uint2 q, bool masked) __attribute__((always_inline)) {
+        auto ld = [&](int blk) __attribute__((always_inline)) {
+            return *reinterpret_cast<const uint2*>(xs + 64 * blk + eoff);
+        };
+        /* one 64-sample block through the MFMAs of groups G0..G1; EX: LPC values exact, else
+         * the bound |T| */
+        auto block = [&](auto g0c, auto g1c, auto exc, uint2 q, bool masked) __attribute__((always_inline)) {
+            constexpr int G0 = decltype(g0c)::value, G1 = decltype(g1c)::value;
+            constexpr bool EX = decltype(exc)::value != 0;
             const h8 A = a_frag(q);
             f4 D[NG + 1];
 #pragma unroll
-            for (int g = 0; g <= NG; ++g) D[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[g], C, 0, 0, 0);
+            for (int g = G0; g <= G1; ++g) D[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[g], C, 0, 0, 0);
 #pragma unroll
-            for (int g = 0; g <= NG; ++g)
+            for (int g = G0; g <= G1; ++g)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     /* (a bit_cast of a vector element reads element 0: clang bug) */
                     const uint32_t bits = __float_as_uint(D[g][r]);
                     if (masked) {
                         const int i = 4 * (4 * kb + r) + rho; /* block 0 */
-                        const uint32_t sv = g == 0 ? sad32(bits, mbv, 0u) : sad32(bits >> shg[g], kg[g], 0u);
+                        const uint32_t sv =
+                            (g == 0 || !EX) ? sad32(bits, mbv, 0u) : sad32(bits >> shg[g], kg[g], 0u);
                         acc[g] += i >= startg[g] ? sv : 0u;
-                    } else if (g == 0) { /* opaque: one v_sad_u32 per value, not a reassociated min/max/sub */
-                        acc[0] = opaque(sad32(bits, mbv, acc[0]));
+                    } else if (g == 0 || !EX) { /* opaque: one v_sad_u32 per value, not a reassociated min/max/sub */
+                        acc[g] = opaque(sad32(bits, mbv, acc[g]));
                     } else {
                         acc[g] = sad32(bits >> shg[g], kg[g], acc[g]);
                     }
                 }
         };
-        /* this wave's blocks wid, wid + nw, ... (wave 0 takes block 0 masked, last); two
-         * blocks per step with both operand reads issued first */
-        int blk = wid == 0 ? nw : wid;
-#if FLACMI_STREAM_UNROLL2
-        for (; blk + nw < nblk; blk += 2 * nw) {
-            const uint2 q0 = *reinterpret_cast<const uint2*>(xs + 64 * blk + eoff);
-            const uint2 q1 = *reinterpret_cast<const uint2*>(xs + 64 * (blk + nw) + eoff);
-            block(q0, false);
-            block(q1, false);
-        }
-#endif
-        for (; blk < nblk; blk += nw) block(*reinterpret_cast<const uint2*>(xs + 64 * blk + eoff), false);
-        if (wid == 0) block(*reinterpret_cast<const uint2*>(xs + eoff), true);
-        /* per (group, order, kb): sum over the 4 phases (quad), lanes with rho == 0 store */
+        /* per (group, order): sum over the 4 phases (quad, < 2^32) then, in 64 bits, over the
+         * 4 kb rows; the lanes with rho == 0 and kb == 0 store */
+        auto reduce_store = [&](auto g0c) __attribute__((always_inline)) {
+            constexpr int G0 = decltype(g0c)::value;
 #pragma unroll
-        for (int g = 0; g <= NG; ++g) {
-            uint32_t v = acc[g];
-            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
-            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
-            v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F); /* lane ^ 16: kb pairs */
-            if (rho == 0 && (kb & 1) == 0) red[(wid * 4 + g) * 8 + o4 * 2 + (kb >> 1)] = v;
+            for (int g = G0; g <= NG; ++g) {
+                uint32_t v = acc[g];
+                v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
+                v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
+                uint64_t w = v;
+                w += (uint64_t)(uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F); /* lane ^ 16 */
+                w += __shfl_xor((unsigned long long)w, 32);
+                if (rho == 0 && kb == 0) red64[(wid * 4 + g) * 4 + o4] = w;
+            }
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using ING = std::integral_constant<int, NG>;
+        /* this wave's blocks wid, wid + nw, ... (wave 0 takes block 0 masked, last) */
+        if (prune) {
+            /* the wave's k-th block runs the LPC groups (bound) for even k */
+            int blk = wid == 0 ? nw : wid;
+            if (wid == 0 && blk < nblk) { /* k = 1 */
+                block(I0{}, I0{}, I0{}, ld(blk), false);
+                blk += nw;
+            }
+            for (; blk + nw < nblk; blk += 2 * nw) {
+                block(I0{}, ING{}, I0{}, ld(blk), false);
+                block(I0{}, I0{}, I0{}, ld(blk + nw), false);
+            }
+            if (blk < nblk) block(I0{}, ING{}, I0{}, ld(blk), false);
+            if (wid == 0) block(I0{}, ING{}, I0{}, ld(0), true);
+#pragma unroll
+            for (int g = 1; g <= NG; ++g) acc[g] >>= shg[g]; /* floor per lane: still a lower bound */
+        } else {
+            for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I0{}, ING{}, I1{}, ld(blk), false);
+            if (wid == 0) block(I0{}, ING{}, I1{}, ld(0), true);
+        }
+        reduce_store(I0{});
+        __syncthreads(); /* B2 */
+        STAMP(3);
+        tj = lane_total();
+        if constexpr (NG > 0) {
+            if (prune) {
+                /* best fixed sum (exact) against every LPC order's lower bound */
+                uint64_t fk = (lane <= 4) ? (tj << 4) | (uint64_t)lane : ~0ull;
+                fk = dpp_min_u64<0xB1>(fk);
+                fk = dpp_min_u64<0x4E>(fk);
+                fk = dpp_min_u64<0x141>(fk);
+                fk = dpp_min_u64<0x140>(fk);
+                const uint64_t fmin = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fk >> 32), 0) << 28) |
+                                      ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fk, 0) >> 4);
+                const uint64_t lb = tj > (uint64_t)n ? tj - (uint64_t)n : 0ull;
+                pruned = __ballot(lane >= 16 && lane < 16 + L && lb <= fmin) == 0;
+                if (!pruned) { /* rare: the exact LPC sums over every block */
+                    __syncthreads(); /* every wave has read the bounds */
+#pragma unroll
+                    for (int g = 1; g <= NG; ++g) acc[g] = 0;
+                    for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I1{}, ING{}, I1{}, ld(blk), false);
+                    if (wid == 0) block(I1{}, ING{}, I1{}, ld(0), true);
+                    reduce_store(I1{});
+                    __syncthreads();
+                    tj = lane_total();
+                }
+            }
         }
     }
-    __syncthreads(); /* B2 */
-    STAMP(3);
     if (a.stop_after == 2) return;
 
     /* ---- choice (encoder.py:331-359, 398-404, 135-157), every wave, lane-parallel ----
      * lanes 0..4: fixed orders 0..4; lanes 16..15+L: LPC orders 1..L.  Key = sum * 16 + index,
      * so a row's minimum key is its smallest sum at the lowest order (python min(): the first
      * minimum); four DPP steps reduce each 16-lane row. */
-    uint64_t tj = 0;
-    {
-        int g = -1, o4 = 0;
-        if (lane >= 1 && lane <= 4) {
-            g = 0;
-            o4 = lane - 1;
-        } else if (NG > 0 && lane >= 16 && lane < 16 + 4 * NG) {
-            g = 1 + ((lane - 16) >> 2);
-            o4 = (lane - 16) & 3;
-        }
-        if (g >= 0) {
-#pragma unroll 1
-            for (int w2 = 0; w2 < nw; ++w2) {
-                const uint2 r2 = *reinterpret_cast<const uint2*>(red + (w2 * 4 + g) * 8 + o4 * 2);
-                tj += (uint64_t)r2.x + r2.y;
-            }
-        } else if (lane == 0) {
-#pragma unroll 1
-            for (int w2 = 0; w2 < nw; ++w2) tj += red0[w2];
-        }
-    }
-    const bool cand = lane <= 4 || (lane >= 16 && lane < 16 + L);
+    const bool cand = lane <= 4 || (!pruned && lane >= 16 && lane < 16 + L);
     uint64_t key = cand ? (tj << 4) | (uint64_t)(lane & 15) : ~0ull;
     key = dpp_min_u64<0xB1>(key);  /* quad_perm [1,0,3,2] */
     key = dpp_min_u64<0x4E>(key);  /* quad_perm [2,3,0,1] */
@@ -510,13 +572,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     uint64_t lsum = 0;
     bool lpc_wins = false, tie = false;
     if constexpr (NG > 0) {
-        const uint64_t lkey = key_at(16);
-        lbest = (int)(lkey & 15) + 1;
-        lsum = lkey >> 4;
-        /* a coefficient-less candidate sums |x| over all n (= the fixed order-0 sum), so it
-         * never wins strictly */
-        lpc_wins = lsum < fsum;
-        tie = !lpc_wins && !(fsum < lsum);
+        if (pruned) {
+            lbest = FLACMI_LPC_PRUNED;
+            lsum = (uint64_t)(int64_t)FLACMI_LPC_PRUNED;
+        } else {
+            const uint64_t lkey = key_at(16);
+            lbest = (int)(lkey & 15) + 1;
+            lsum = lkey >> 4;
+            /* a coefficient-less candidate sums |x| over all n (= the fixed order-0 sum), so it
+             * never wins strictly */
+            lpc_wins = lsum < fsum;
+            tie = !lpc_wins && !(fsum < lsum);
+        }
     }
     if (wid == 0 && a.fixed_sums && lane < 5) a.fixed_sums[gid * 5 + lane] = (long long)tj;
     if (wid == 0 && a.lpc_sums) {
@@ -813,6 +880,7 @@ hipError_t launch_resid_stream(const ResidArgs& a, hipStream_t s) {
     else if (a.L <= 8) e = launch_stream_T<2>(a, s);
     else e = launch_stream_T<3>(a, s);
     if (e != hipSuccess) return e;
+    if ((e = launch_poison_lds(s)) != hipSuccess) return e;
     return a.L <= 8 ? launch_resid_retry_l8(a, s) : launch_resid_retry_l12(a, s);
 }
 

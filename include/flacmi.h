@@ -116,8 +116,23 @@ typedef struct flacmi_params {
     int32_t rice_min;        /* rice_partition_order.start */
     int32_t rice_max;        /* rice_partition_order.stop - 1 (rice_max < rice_min: empty range) */
     int32_t mode;            /* flacmi_mode */
-    int32_t reserved[3];     /* reserved[0]: predictor order in FLACMI_MODE_RICE_ONLY, else 0 */
+    int32_t reserved[3];     /* reserved[0]: predictor order in FLACMI_MODE_RICE_ONLY, else 0;
+                                reserved[1]: flacmi_flags; reserved[2]: 0 */
 } flacmi_params;
+
+/* params.reserved[1] bits */
+enum flacmi_flags {
+    /* compute every LPC candidate's exact sum(|r|) in FLACMI_MODE_REFERENCE (meta.lpc_order /
+     * lpc_sum always exact).  Without it the analysis may prune: see FLACMI_LPC_PRUNED. */
+    FLACMI_FLAG_ALL_CANDIDATES = 1,
+};
+
+/* meta.lpc_order and meta.lpc_sum of a unit whose LPC candidates were pruned: exact lower
+ * bounds proved every candidate's sum(|r|) strictly above the best fixed sum, so the
+ * reference's choice (encoder.py:135-157) is the fixed subframe and no tie is possible.
+ * Everything the reference writes (kind, order, residual, Rice fields) is unaffected.  Runs
+ * with outputs.lpc_sums or FLACMI_FLAG_ALL_CANDIDATES never prune. */
+#define FLACMI_LPC_PRUNED (-1)
 
 /* One batch of units.  Samples are planar: unit u occupies
  * samples[u*unit_stride .. u*unit_stride + len(u)).  Every unit has `block_len`
@@ -151,13 +166,13 @@ typedef struct flacmi_unit_meta {
     int32_t res_offset;      /* first valid element of the residual row */
     int32_t res_len;         /* len(residual) */
     int32_t fixed_order;     /* best fixed order 0..4 */
-    int32_t lpc_order;       /* best LPC order 1..L (0 in fixed-only mode) */
+    int32_t lpc_order;       /* best LPC order 1..L (0 in fixed-only mode, FLACMI_LPC_PRUNED if pruned) */
     int32_t part_order;      /* Residual.partition_order as chosen by rice_partitions */
     int32_t n_parts;         /* len(Residual.partitions) */
     int32_t coding_method;   /* RiceCodingMethod value: 4 or 5 */
     int32_t reserved0;
     int64_t fixed_sum;       /* sum(|r|) of the best fixed residual */
-    int64_t lpc_sum;         /* sum(|r|) of the best LPC residual (0 in fixed-only mode) */
+    int64_t lpc_sum;         /* sum(|r|) of the best LPC residual (0 in fixed-only mode, FLACMI_LPC_PRUNED if pruned) */
     int64_t rice_bits;       /* size estimate of the chosen partitioning (encoder.py:714-727) */
     int32_t coefs[FLACMI_MAX_LPC_ORDER];
 } flacmi_unit_meta;
@@ -345,7 +360,9 @@ int flacmi_decode_frames_device(flacmi_ctx* ctx, const uint8_t* stream_data, int
 #define FLACMI_STATS_WORDS 128
 /* stats[0] units, [1] samples, [2] rice bits, [3] fixed units, [4] lpc units,
  * [5..9] fixed order histogram, [10..42] lpc order histogram (index 10+order-1... 41),
- * [48..63] partition order histogram, [64..79] status histogram, [80] residual checksum */
+ * [48..63] partition order histogram, [64..79] status histogram, [80] checksum of the units'
+ * (rice_bits, fixed_sum, kind, order): results that do not depend on LPC pruning; [81] units whose
+ * LPC candidates were pruned (FLACMI_LPC_PRUNED) */
 int flacmi_stream_stats(flacmi_ctx* ctx, const flacmi_unit_meta* d_meta, int64_t n_units,
                         int32_t block_len, int32_t tail_len, int64_t n_tail_units,
                         int64_t* d_stats, void* stream);

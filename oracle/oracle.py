@@ -136,6 +136,29 @@ def analyze_batch(samples2d: np.ndarray, params: abi.Params, block_len: int, tai
             "lpc_sums": ls, "lpc_records": rec}
 
 
+def meta_mismatches(dev, ora) -> list:
+    """Fields of a device meta row (abi.META_DTYPE) that differ from the oracle's row.  A
+    device row with lpc_order == abi.LPC_PRUNED (the analysis proved every LPC candidate
+    loses, include/flacmi.h FLACMI_LPC_PRUNED) must have lpc_sum == LPC_PRUNED, and the
+    oracle must agree that LPC loses strictly: its best LPC sum above its best fixed sum."""
+    bad = []
+    pruned = int(dev["lpc_order"]) == abi.LPC_PRUNED
+    for f in abi.META_DTYPE.names:
+        if f in ("coefs", "reserved0") or (pruned and f in ("lpc_order", "lpc_sum")):
+            continue
+        if dev[f] != ora[f]:
+            bad.append((f, dev[f], ora[f]))
+    k = int(ora["ncoefs"])
+    if list(dev["coefs"][:k]) != list(ora["coefs"][:k]):
+        bad.append(("coefs", list(dev["coefs"][:k]), list(ora["coefs"][:k])))
+    if pruned:
+        if int(dev["lpc_sum"]) != abi.LPC_PRUNED:
+            bad.append(("lpc_sum (pruned)", int(dev["lpc_sum"]), abi.LPC_PRUNED))
+        if int(ora["status"]) == 0 and not int(ora["lpc_sum"]) > int(ora["fixed_sum"]):
+            bad.append(("pruned but LPC does not lose", int(ora["lpc_sum"]), int(ora["fixed_sum"])))
+    return bad
+
+
 def tukey(n: int):
     w = np.zeros(max(n, 1), dtype=np.float64)
     st = lib().oracle_tukey(n, _ptr(w, C.c_double))

@@ -26,8 +26,9 @@ def stream_stats(meta, block_len, tail_len=0, n_tail_units=0):
             h[4] += 1
             h[9 + (order if 1 <= order <= 32 else 32)] += 1
         h[48 + (int(m["part_order"]) & 15)] += 1
+        h[81] += int(m["lpc_order"]) == -1
         hsh = ((int(m["rice_bits"]) * 0x9E3779B97F4A7C15) & M64) ^ ((int(m["fixed_sum"]) << 1) & M64) ^ \
-            (int(m["lpc_sum"]) & M64)
+            (((int(m["kind"]) * 64 + order) * 0xD1B54A32D192ED03) & M64)
         h[80] = (h[80] + hsh) & M64
     out = np.array([v if v < (1 << 63) else v - (1 << 64) for v in h], dtype=np.int64)
     return out

@@ -61,17 +61,16 @@ def test_device_matches_reference_golden(az, entry):
 # ---------------------------------------------------------------------------------------
 def compare_with_oracle(out, ora, lens):
     gm, om = out["meta"], ora["meta"]
-    fields = [f for f in abi.META_DTYPE.names if f not in ("coefs", "reserved0")]
     for u, n in enumerate(lens):
         st = int(om["status"][u])
         assert int(gm["status"][u]) == st, (u, "status", int(gm["status"][u]), st)
         assert int(gm["site"][u]) == int(om["site"][u]), (u, "site")
         if st != 0:
             continue
-        for f in fields:
-            assert gm[f][u] == om[f][u], (u, f, gm[f][u], om[f][u])
-        k = int(om["ncoefs"][u])
-        assert list(gm["coefs"][u][:k]) == list(om["coefs"][u][:k]), (u, "coefs")
+        bad = oracle.meta_mismatches(gm[u], om[u])
+        assert not bad, (u, bad)
+        if "lpc_sums" in out:  # debug runs never prune
+            assert int(gm["lpc_order"][u]) != abi.LPC_PRUNED, (u, "pruned in a debug run")
         npart = int(om["n_parts"][u])
         assert np.array_equal(out["rice_params"][u][:npart], ora["rice_params"][u][:npart]), (u, "params")
         off, ln = int(om["res_offset"][u]), int(om["res_len"][u])
@@ -411,11 +410,16 @@ def test_fast_kernel_stages_the_whole_record(az, rmin, rmax):
 
 
 def _meta_params_residual_equal(a, b, u):
+    """a: production run (may prune), b: a run with every LPC candidate's exact sum."""
     am, bm = a["meta"], b["meta"]
+    pruned = int(am["lpc_order"][u]) == abi.LPC_PRUNED
     for f in abi.META_DTYPE.names:
-        if f == "reserved0":
+        if f == "reserved0" or (pruned and f in ("lpc_order", "lpc_sum")):
             continue
         assert np.array_equal(am[f][u], bm[f][u]), (u, f, am[f][u], bm[f][u])
+    if pruned:
+        assert int(am["lpc_sum"][u]) == abi.LPC_PRUNED
+        assert int(bm["kind"][u]) == abi.KIND_FIXED and int(bm["lpc_sum"][u]) > int(bm["fixed_sum"][u]), u
     if int(am["status"][u]) == 0:
         k = int(am["n_parts"][u])
         assert np.array_equal(a["rice_params"][u][:k], b["rice_params"][u][:k]), (u, "params")
@@ -453,3 +457,75 @@ def test_production_call_near_tied_orders_vs_oracle(az, q):
     out = az.analyze(a, make_params(12, q, 0, 5), n, sample_bits=16, debug=False)
     ora = oracle.analyze_batch(a, oracle.make_params(12, q, 0, 5), n, sample_bits=16, threads=16)
     compare_with_oracle(out, ora, [n] * len(a))
+
+
+def _outside_stream_bound(ora, L, limit=127):
+    """Units with an LPC order outside k_resid_stream's MFMA exactness bound
+    (sum|c| + 2^shift > 127): the stream kernel lists them for k_resid's list variant."""
+    cnt = 0
+    for rec in ora["lpc_records"]:
+        if rec[0] != 0:
+            continue
+        for p in range(1, L + 1):
+            base = 2 + 32 + p * (p - 1) // 2
+            if int(np.abs(rec[base: base + p].astype(np.int64)).sum()) + (1 << int(rec[2 + p - 1])) > limit:
+                cnt += 1
+                break
+    return cnt
+
+
+@pytest.mark.parametrize("q", [7, 8, 9])
+@pytest.mark.parametrize("debug", [True, False])
+def test_stream_retry_list_above_6144(az, q, debug):
+    """n = 8192 takes k_resid_stream (n <= 10240) while the retry list's k_resid variant keeps
+    its residual in LDS (n > 8 * kCPT * 256): the list launch must size its LDS the way that
+    variant carves it (it used the register-resident layout).  Some units must
+    actually be retried."""
+    n, nu = 8192, 48
+    a = oracle.synth_batch(0, nu, n, 16, 8000 + q, dtype=np.int16)
+    ora = oracle.analyze_batch(a, oracle.make_params(12, q, 0, 5), n, sample_bits=16, threads=16)
+    assert _outside_stream_bound(ora, 12) > 0
+    out = az.analyze(a, make_params(12, q, 0, 5), n, sample_bits=16, debug=debug)
+    compare_with_oracle(out, ora, [n] * nu)
+
+
+def _prune_signals(n, seed):
+    """Units on every side of the LPC lower bound: config-2 synthetic units (pruned), AR(1)
+    noise (LPC within 1.3x of fixed: the half-block bound fails, the exact pass runs and
+    fixed wins), white noise (LPC wins or loses by a few units) and tones."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n)
+    rows = [oracle.synth_batch(0, 24, n, 16, seed, dtype=np.int16)]
+    x = []
+    for u in range(8):
+        w = rng.normal(0, 2000, n)
+        ar = w.copy()
+        ar[1:] += (0.9 if u % 2 else -0.7) * w[:-1]
+        x += [ar, rng.integers(-3000, 3000, n), 8000 * np.sin(2 * np.pi * (u + 1) * 37 / n * t) + rng.normal(0, 40, n)]
+    rows.append(np.clip(np.round(np.array(x)), -32768, 32767).astype(np.int16))
+    return np.concatenate(rows)
+
+
+@pytest.mark.parametrize("q", [5, 9, 15])
+def test_lpc_pruning_paths_vs_oracle(az, q):
+    """Production calls prune LPC candidates whose lower bound already loses (include/flacmi.h
+    FLACMI_LPC_PRUNED): every reference-visible field equals the oracle on pruned units, on
+    units where the bound fails and the exact pass decides for fixed, and on LPC-chosen units;
+    FLACMI_FLAG_ALL_CANDIDATES gives the exact LPC sums with the same results."""
+    n = 4608
+    a = _prune_signals(n, 50 + q)
+    ora = oracle.analyze_batch(a, oracle.make_params(12, q, 0, 5), n, sample_bits=16, threads=16)
+    prod = az.analyze(a, make_params(12, q, 0, 5), n, sample_bits=16)
+    full = az.analyze(a, make_params(12, q, 0, 5, all_candidates=True), n, sample_bits=16)
+    compare_with_oracle(prod, ora, [n] * len(a))
+    compare_with_oracle(full, ora, [n] * len(a))
+    pm, om = prod["meta"], ora["meta"]
+    assert not (full["meta"]["lpc_order"] == abi.LPC_PRUNED).any()
+    for u in range(len(a)):
+        _meta_params_residual_equal(prod, full, u)
+    ok = om["status"] == 0
+    pruned = pm["lpc_order"] == abi.LPC_PRUNED
+    if q == 5:  # (at q >= 9 these units exceed k_resid_stream's MFMA bound: k_resid never prunes)
+        assert pruned[:24].sum() >= 12, "config-2 units should mostly prune"
+    assert (ok & ~pruned & (om["kind"] == abi.KIND_FIXED)).any(), "no unit took the exact pass and chose fixed"
+    assert (ok & (om["kind"] == abi.KIND_LPC)).any(), "no LPC-chosen unit"
