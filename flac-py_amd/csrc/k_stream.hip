@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     {
         const int col = lane & 15, kb = lane >> 4, o4 = col >> 2, rho = col & 3;
         h8 B[NG + 1];
-        int shg[NG + 1], startg[NG + 1];
+        int shg[NG + 1];
         uint32_t kg[NG + 1];
         const int idx0 = 12 + rho - 4 * kb + 2; /* tap index of the lane's first operand pair, + 2 */
 #pragma unroll
@@ -436,16 +436,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                 const uint32_t hh = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[2], 256.0f * t[3]));
                 B[g] = __builtin_bit_cast(h8, uint4{h0, hh, l0, l2});
             }
-            int sh = 0, start = o4 + 1;
+            int sh = 0;
             if (g > 0) {
                 const int p = 4 * (g - 1) + o4 + 1;
                 sh = p <= L ? recl[2 + p - 1] : 0;
-                start = ((negmask >> (p - 1)) & 1) ? 0 : p;
             }
             shg[g] = sh;
             kg[g] = kMagicBits >> sh;
-            startg[g] = start;
         }
+        /* first residual index of group g's order at this lane (block 0 only) */
+        auto start_of = [&](int g) __attribute__((always_inline)) -> int {
+            const int p = 4 * (g > 0 ? g - 1 : 0) + o4 + 1;
+            return (g > 0 && ((negmask >> (p - 1)) & 1)) ? 0 : p;
+        };
         const uint32_t mbv = opaque(kMagicBits);
         const f4 C{12582912.0f, 12582912.0f, 12582912.0f, 12582912.0f};
         const int eoff = 4 * (lane & 15) - 12 + 4 * kb;
@@ -457,10 +460,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         };
         /* one 64-sample block through the MFMAs of groups G0..G1; EX: LPC values exact, else
          * the bound |T| */
-        auto block = [&](auto g0c, auto g1c, auto exc, uint2 q, bool masked) __attribute__((always_inline)) {
+        auto blockA = [&](auto g0c, auto g1c, auto exc, const h8 A, bool masked) __attribute__((always_inline)) {
             constexpr int G0 = decltype(g0c)::value, G1 = decltype(g1c)::value;
             constexpr bool EX = decltype(exc)::value != 0;
-            const h8 A = a_frag(q);
             f4 D[NG + 1];
 #pragma unroll
             for (int g = G0; g <= G1; ++g) D[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[g], C, 0, 0, 0);
@@ -474,7 +476,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                         const int i = 4 * (4 * kb + r) + rho; /* block 0 */
                         const uint32_t sv =
                             (g == 0 || !EX) ? sad32(bits, mbv, 0u) : sad32(bits >> shg[g], kg[g], 0u);
-                        acc[g] += i >= startg[g] ? sv : 0u;
+                        acc[g] += i >= start_of(g) ? sv : 0u;
                     } else if (g == 0 || !EX) { /* opaque: one v_sad_u32 per value, not a reassociated min/max/sub */
                         acc[g] = opaque(sad32(bits, mbv, acc[g]));
                     } else {
@@ -482,13 +484,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                     }
                 }
         };
+        auto block = [&](auto g0c, auto g1c, auto exc, uint2 q, bool masked) __attribute__((always_inline)) {
+            blockA(g0c, g1c, exc, a_frag(q), masked);
+        };
         /* per (group, order): sum over the 4 phases (quad, < 2^32) then, in 64 bits, over the
-         * 4 kb rows; the lanes with rho == 0 and kb == 0 store */
-        auto reduce_store = [&](auto g0c) __attribute__((always_inline)) {
+         * 4 kb rows; the lanes with rho == 0 and kb == 0 store.  BD: the LPC groups hold the
+         * bound sum |T|, stored as floor(acc / 2^shift) per lane (a lower bound of the sum of
+         * |T| / 2^shift; acc itself keeps accumulating over later tiers) */
+        auto reduce_store = [&](auto g0c, auto bdc) __attribute__((always_inline)) {
             constexpr int G0 = decltype(g0c)::value;
+            constexpr bool BD = decltype(bdc)::value != 0;
 #pragma unroll
             for (int g = G0; g <= NG; ++g) {
-                uint32_t v = acc[g];
+                uint32_t v = (BD && g > 0) ? acc[g] >> shg[g] : acc[g];
                 v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
                 v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);
                 uint64_t w = v;
@@ -500,27 +508,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
         using ING = std::integral_constant<int, NG>;
-        /* this wave's blocks wid, wid + nw, ... (wave 0 takes block 0 masked, last) */
+        /* this wave's blocks wid + k nw, k = 0 .. kw - 1 (wave 0 takes block 0 masked, last) */
+        const int kw = (nblk - wid + nw - 1) / nw;
         if (prune) {
-            /* the wave's k-th block runs the LPC groups (bound) for even k */
-            int blk = wid == 0 ? nw : wid;
-            if (wid == 0 && blk < nblk) { /* k = 1 */
-                block(I0{}, I0{}, I0{}, ld(blk), false);
-                blk += nw;
+            /* tier 0: the wave's blocks k % 4 == 0 run the LPC groups (bound) beside the fixed
+             * group; tiers 1..3 (only while the bound has not decided) add k % 4 == 2, 1, 3 */
+            for (int k = wid == 0 ? 1 : 0; k < kw; ++k) {
+                const h8 A = a_frag(ld(wid + k * nw));
+                blockA(I0{}, I0{}, I0{}, A, false);
+                if ((k & 3) == 0) blockA(I1{}, ING{}, I0{}, A, false);
             }
-            for (; blk + nw < nblk; blk += 2 * nw) {
-                block(I0{}, ING{}, I0{}, ld(blk), false);
-                block(I0{}, I0{}, I0{}, ld(blk + nw), false);
-            }
-            if (blk < nblk) block(I0{}, ING{}, I0{}, ld(blk), false);
             if (wid == 0) block(I0{}, ING{}, I0{}, ld(0), true);
-#pragma unroll
-            for (int g = 1; g <= NG; ++g) acc[g] >>= shg[g]; /* floor per lane: still a lower bound */
+            reduce_store(I0{}, I1{});
         } else {
             for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I0{}, ING{}, I1{}, ld(blk), false);
             if (wid == 0) block(I0{}, ING{}, I1{}, ld(0), true);
+            reduce_store(I0{}, I0{});
         }
-        reduce_store(I0{});
         __syncthreads(); /* B2 */
         STAMP(3);
         tj = lane_total();
@@ -534,15 +538,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                 fk = dpp_min_u64<0x140>(fk);
                 const uint64_t fmin = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(fk >> 32), 0) << 28) |
                                       ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fk, 0) >> 4);
-                const uint64_t lb = tj > (uint64_t)n ? tj - (uint64_t)n : 0ull;
-                pruned = __ballot(lane >= 16 && lane < 16 + L && lb <= fmin) == 0;
+#pragma unroll 1
+                for (int t = 1;; ++t) {
+                    const uint64_t lb = tj > (uint64_t)n ? tj - (uint64_t)n : 0ull;
+                    pruned = __ballot(lane >= 16 && lane < 16 + L && lb <= fmin) == 0;
+                    if (pruned || t == 4) break;
+                    /* the next quarter of the blocks (k % 4 == 2, 1, 3; block 0 is in tier 0) */
+                    __syncthreads(); /* every wave has read the bounds */
+                    for (int k = t == 1 ? 2 : t == 2 ? 1 : 3; k < kw; k += 4) block(I1{}, ING{}, I0{}, ld(wid + k * nw), false);
+                    reduce_store(I1{}, I1{});
+                    __syncthreads();
+                    tj = lane_total();
+                }
                 if (!pruned) { /* rare: the exact LPC sums over every block */
                     __syncthreads(); /* every wave has read the bounds */
 #pragma unroll
                     for (int g = 1; g <= NG; ++g) acc[g] = 0;
                     for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I1{}, ING{}, I1{}, ld(blk), false);
                     if (wid == 0) block(I1{}, ING{}, I1{}, ld(0), true);
-                    reduce_store(I1{});
+                    reduce_store(I1{}, I0{});
                     __syncthreads();
                     tj = lane_total();
                 }
