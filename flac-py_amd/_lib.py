@@ -14,7 +14,9 @@ _lib = None
 
 
 class FlacmiError(RuntimeError):
-    """A libflacmi.so API call failed (argument, HIP runtime or unsupported shape)."""
+    """A libflacmi.so API call failed (argument, HIP runtime or unsupported shape); `code`
+    is the FLACMI_E_* return value when there is one."""
+    code = None
 
 
 def load() -> C.CDLL:
@@ -45,7 +47,9 @@ def load() -> C.CDLL:
 def check(rc: int, what: str = "flacmi") -> None:
     if rc != 0:
         msg = load().flacmi_last_error().decode(errors="replace")
-        raise FlacmiError(f"{what} failed ({rc}): {msg}")
+        err = FlacmiError(f"{what} failed ({rc}): {msg}")
+        err.code = rc
+        raise err
 
 
 def last_error() -> str:

@@ -215,6 +215,8 @@ SIGNATURES = {
                                          C.POINTER(EncodeTiming)]),
     "flacmi_host_register": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     "flacmi_host_unregister": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "flacmi_host_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),
+    "flacmi_host_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "flacmi_decode_frames_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
                                               C.POINTER(DecodeParams), C.POINTER(Batch), C.c_void_p, C.c_int64,
                                               C.c_void_p, C.c_void_p, C.c_void_p]),

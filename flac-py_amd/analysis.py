@@ -8,6 +8,7 @@ include/flacmi.h).  `analyze_device()` is the zero-copy form on device pointers 
 bench.py.
 """
 import ctypes as C
+import weakref
 
 import numpy as np
 
@@ -211,6 +212,8 @@ class Analyzer:
             raise ValueError("samples must be a 2-D int16 or int32 array with contiguous rows")
         if s.strides[0] % s.itemsize:
             raise ValueError("the row stride must be a whole number of samples")
+        if s.shape[1] < max(block_len, tail_len if n_tail_units else 0):
+            raise ValueError(f"rows hold {s.shape[1]} samples, fewer than the block length")
         n_units = s.shape[0]
         b = abi.Batch()
         b.samples = s.ctypes.data
@@ -252,6 +255,20 @@ class Analyzer:
 
     def host_unregister(self, a: np.ndarray) -> None:
         check(self.lib.flacmi_host_unregister(self.ctx, a.ctypes.data), "flacmi_host_unregister")
+
+    def host_array(self, shape, dtype) -> np.ndarray:
+        """A numpy array over page-locked host memory (flacmi_host_alloc), freed with the
+        array: staging rows and frame buffers reused call after call without page-locking."""
+        dt = np.dtype(dtype)
+        count = int(np.prod(shape)) if len(shape) else 1
+        nbytes = max(count * dt.itemsize, 1)
+        p = self.lib.flacmi_host_alloc(self.ctx, nbytes)
+        if not p:
+            raise FlacmiError(f"flacmi_host_alloc({nbytes}): {self.lib.flacmi_last_error().decode(errors='replace')}")
+        raw = (C.c_uint8 * nbytes).from_address(p)
+        a = np.frombuffer(raw, dtype=dt, count=count).reshape(shape)
+        weakref.finalize(a, self.lib.flacmi_host_free, None, p)  # valid after close() too
+        return a
 
     def frame_sizes_device(self, batch: abi.Batch, fp: abi.FrameParams, meta_ptr: int, params_ptr: int,
                            params_stride: int, offsets_ptr: int, status_ptr: int, stream: int = 0) -> None:

@@ -1,10 +1,12 @@
 """Command line with flac/__main__.py's `encode` action (its arguments, defaults and
-output bytes), on the device path: streamed PCM ingest (ingest.iter_wav_batches, the
+output bytes), on the device path: streamed PCM ingest (ingest.iter_wav_pcm, the
 reference reader's byte grouping unless --correct-reader), device analysis and device
-frame writer (encoder.encode_wav).
+frame writer through the streaming pipeline (encoder.encode_wav); --devices spreads the
+batches over several GPUs.
 
     python -m flac_amd encode infile.wav outfile.flac [-b N] [-l N] [-q N] [-r [M,]N]
                                                        [--correct-reader] [--fixed-only]
+                                                       [--device N | --devices N,M,...]
 
 The reference's `decode` action (a WAV writer over its host decoder) is not part of this
 build; the device decoder (flacmi_decode_frames_device) is a frame verifier.
@@ -37,6 +39,8 @@ def make_argument_parser():
                      help="read sampwidth-byte samples (the reference groups frame bytes by channel count)")
     enc.add_argument("--fixed-only", action="store_true", help="fixed predictors only (BASELINE config 5)")
     enc.add_argument("--device", type=int, default=0)
+    enc.add_argument("--devices", type=lambda v: [int(x) for x in v.split(",")], default=None, metavar="N,M,...",
+                     help="encode on these devices, batches round-robin (frames in block order)")
     return parser
 
 
@@ -48,7 +52,7 @@ def cmd_encode(args) -> None:
     t0 = timer()
     with args.outfile.open("wb") as f:
         for bs in encode_wav(args.infile, parameters, quirk=not args.correct_reader, device=args.device,
-                             fixed_only=args.fixed_only):
+                             devices=args.devices, fixed_only=args.fixed_only):
             f.write(bs)
     print(f"Encoding completed in {timer() - t0:.6g} seconds")
 

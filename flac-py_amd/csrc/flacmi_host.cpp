@@ -170,7 +170,9 @@ struct flacmi_ctx {
     hipStream_t side = nullptr;          /* k_lpc stream of the overlap mode */
     hipEvent_t lpc_done[kMaxChunks] = {}; /* k_lpc of chunk i finished (no timing) */
     int ncalls = 0; /* calls since the last timing reset */
+    struct EncState* enc = nullptr; /* flacmi_encode_pipeline's streams, slots and pinned arrays */
 };
+static void enc_free(struct EncState* es);
 
 static int ensure_buf(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return 0;
@@ -247,6 +249,7 @@ void flacmi_destroy(flacmi_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
+    enc_free(ctx->enc);
     for (auto& kv : ctx->windows) (void)hipFree(kv.second);
     for (DevBuf* b : {&ctx->slow, &ctx->dec, &ctx->rec, &ctx->retry, &ctx->h_samples, &ctx->h_meta, &ctx->h_params, &ctx->h_residual, &ctx->h_acf,
                       &ctx->h_fs, &ctx->h_ls, &ctx->h_recs, &ctx->scan, &ctx->h_offsets, &ctx->h_status,
@@ -865,21 +868,27 @@ int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_
 }
 
 /* ---- pipelined host encode ---------------------------------------------------------
- * Streams: `cs` (compute: analysis, sizes, pack, in order, so the context's shared scratch
- * is never used by two launches at once), `is` (host -> device) and `os` (device -> host).
- * Per sub-batch k (slot k % kEncSlots):
- *   front(k): is: H2D rows -> cs: analyze, frame sizes -> os: offsets/status D2H (pinned)
+ * Streams: `cs` (compute: analysis, sizes, the small offsets/status copy back, pack, in
+ * order, so the context's shared scratch is never used by two launches at once), `is`
+ * (host -> device samples) and `os` (device -> host frame bytes).  Per sub-batch k (slot
+ * k % kEncSlots):
+ *   front(k): is: H2D rows -> cs: analyze, frame sizes, offsets/status D2H (pinned)
  *   back(k):  host waits for those offsets, then cs: pack -> os: frame bytes D2H into out
  * issued as front(0), front(1), back(0), front(2), back(1), ... so the copies of one
- * sub-batch run under the kernels of the others. */
+ * sub-batch run under the kernels of the others.  The offsets of k ride the compute stream:
+ * on `os` they would queue behind the frame bytes of k - 1 and the host would wait for that
+ * copy before issuing the next H2D (the two copy directions then ran back to back).
+ * Streams, events, slot buffers and the pinned offset arrays live in the context and grow
+ * as needed (ensure_buf), so streaming many calls pays no setup. */
 namespace {
+constexpr int kEncSlots = 3;
 struct EncSlot {
     DevBuf samples, meta, params, residual, offsets, status, frames;
     int64_t* h_off = nullptr;   /* pinned: frame offsets of the sub-batch */
     int32_t* h_st = nullptr;    /* pinned: frame status */
     hipEvent_t e[9] = {};       /* h2d start/end, analyze end, sizes end, pack start/end, d2h start/end, offsets copied */
     flacmi_batch b{};
-    int64_t first_unit = 0, nf = 0, total = 0;
+    int64_t first_unit = 0, nf = 0, total = 0, dstride = 0;
     int rbytes = 4;
 };
 float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -888,11 +897,66 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 }
 }  // namespace
 
+struct EncState {
+    hipStream_t cs = nullptr, is = nullptr, os = nullptr;
+    EncSlot slot[kEncSlots];
+    int64_t cap_nf = 0; /* frames the pinned arrays of each slot hold */
+};
+
+static void enc_free(EncState* es) {
+    if (!es) return;
+    for (hipStream_t st : {es->cs, es->is, es->os})
+        if (st) (void)hipStreamSynchronize(st);
+    for (auto& sl : es->slot) {
+        for (DevBuf* d : {&sl.samples, &sl.meta, &sl.params, &sl.residual, &sl.offsets, &sl.status, &sl.frames})
+            if (d->p) (void)hipFree(d->p);
+        if (sl.h_off) (void)hipHostFree(sl.h_off);
+        if (sl.h_st) (void)hipHostFree(sl.h_st);
+        for (auto& e : sl.e)
+            if (e) (void)hipEventDestroy(e);
+    }
+    for (hipStream_t st : {es->cs, es->is, es->os})
+        if (st) (void)hipStreamDestroy(st);
+    delete es;
+}
+
+static int enc_state(flacmi_ctx* ctx, int64_t per_nf, EncState** out) {
+    if (!ctx->enc) {
+        EncState* es = new EncState();
+        ctx->enc = es;
+        HIP_TRY(hipStreamCreateWithFlags(&es->cs, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&es->is, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&es->os, hipStreamNonBlocking));
+        for (auto& sl : es->slot)
+            for (auto& e : sl.e) HIP_TRY(hipEventCreate(&e));
+    }
+    EncState* es = ctx->enc;
+    if (es->cap_nf < per_nf) {
+        for (auto& sl : es->slot) {
+            if (sl.h_off) HIP_TRY(hipHostFree(sl.h_off));
+            if (sl.h_st) HIP_TRY(hipHostFree(sl.h_st));
+            sl.h_off = nullptr;
+            sl.h_st = nullptr;
+        }
+        es->cap_nf = 0;
+        for (auto& sl : es->slot) {
+            HIP_TRY(hipHostMalloc((void**)&sl.h_off, sizeof(int64_t) * (per_nf + 1), hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&sl.h_st, sizeof(int32_t) * per_nf, hipHostMallocDefault));
+        }
+        es->cap_nf = per_nf;
+    }
+    *out = es;
+    return 0;
+}
+
 static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, const flacmi_params* params,
-                     const flacmi_frame_params* fp, hipStream_t cs, hipStream_t is, hipStream_t os) {
+                     const flacmi_frame_params* fp, hipStream_t cs, hipStream_t is) {
     const flacmi_batch& b = sl.b;
     const size_t nu = (size_t)b.n_units;
-    const int64_t sstride = ((b.block_len * b.sample_bytes + 15) / 16) * 16 / b.sample_bytes;
+    /* rows whose stride is a multiple of 16 bytes keep it on the device: one linear copy */
+    const bool linear = (whole->unit_stride * b.sample_bytes) % 16 == 0;
+    sl.dstride = linear ? whole->unit_stride : ((b.block_len * b.sample_bytes + 15) / 16) * 16 / b.sample_bytes;
+    const int64_t sstride = sl.dstride;
     const int64_t pstride = (1LL << (params->rice_max > 0 ? params->rice_max : 0)) + 1;
     const int64_t rstride = ((b.block_len * sl.rbytes + 15) / 16) * 16 / sl.rbytes;
     if (int rc = ensure_buf(sl.samples, nu * sstride * b.sample_bytes)) return rc;
@@ -901,11 +965,14 @@ static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, co
     if (int rc = ensure_buf(sl.residual, nu * rstride * sl.rbytes)) return rc;
     if (int rc = ensure_buf(sl.offsets, sizeof(int64_t) * (size_t)(sl.nf + 1))) return rc;
     if (int rc = ensure_buf(sl.status, sizeof(int32_t) * (size_t)sl.nf)) return rc;
+    const uint8_t* src = (const uint8_t*)whole->samples + sl.first_unit * whole->unit_stride * b.sample_bytes;
     HIP_TRY(hipEventRecord(sl.e[0], is));
-    HIP_TRY(hipMemcpy2DAsync(sl.samples.p, sstride * b.sample_bytes,
-                             (const uint8_t*)whole->samples + sl.first_unit * whole->unit_stride * b.sample_bytes,
-                             whole->unit_stride * b.sample_bytes, b.block_len * b.sample_bytes, nu,
-                             hipMemcpyHostToDevice, is));
+    if (linear)
+        HIP_TRY(hipMemcpyAsync(sl.samples.p, src, ((nu - 1) * sstride + b.block_len) * b.sample_bytes,
+                               hipMemcpyHostToDevice, is));
+    else
+        HIP_TRY(hipMemcpy2DAsync(sl.samples.p, sstride * b.sample_bytes, src, whole->unit_stride * b.sample_bytes,
+                                 b.block_len * b.sample_bytes, nu, hipMemcpyHostToDevice, is));
     HIP_TRY(hipEventRecord(sl.e[1], is));
     HIP_TRY(hipStreamWaitEvent(cs, sl.e[1], 0));
     flacmi_batch db = b;
@@ -926,10 +993,9 @@ static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, co
     FrameArgs a = frame_args(ctx, &db, &f, o.meta, o.rice_params, pstride, sl.nf);
     if (int rc = frame_sizes_impl(ctx, a, (int64_t*)sl.offsets.p, (int32_t*)sl.status.p, cs)) return rc;
     HIP_TRY(hipEventRecord(sl.e[3], cs));
-    HIP_TRY(hipStreamWaitEvent(os, sl.e[3], 0));
-    HIP_TRY(hipMemcpyAsync(sl.h_off, sl.offsets.p, sizeof(int64_t) * (sl.nf + 1), hipMemcpyDeviceToHost, os));
-    HIP_TRY(hipMemcpyAsync(sl.h_st, sl.status.p, sizeof(int32_t) * sl.nf, hipMemcpyDeviceToHost, os));
-    HIP_TRY(hipEventRecord(sl.e[8], os));
+    HIP_TRY(hipMemcpyAsync(sl.h_off, sl.offsets.p, sizeof(int64_t) * (sl.nf + 1), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(sl.h_st, sl.status.p, sizeof(int32_t) * sl.nf, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipEventRecord(sl.e[8], cs));
     return 0;
 }
 
@@ -944,6 +1010,29 @@ extern "C" int flacmi_host_unregister(flacmi_ctx* ctx, void* ptr) {
     if (!ctx || !ptr) return fail(FLACMI_E_INVALID, "null context or pointer");
     if (int rc = set_device(ctx)) return rc;
     HIP_TRY(hipHostUnregister(ptr));
+    return 0;
+}
+
+extern "C" void* flacmi_host_alloc(flacmi_ctx* ctx, size_t bytes) {
+    if (!ctx || bytes == 0) {
+        fail(FLACMI_E_INVALID, "null context or empty range");
+        return nullptr;
+    }
+    if (set_device(ctx)) return nullptr;
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        fail(FLACMI_E_NOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+extern "C" int flacmi_host_free(flacmi_ctx* ctx, void* ptr) {
+    if (!ptr) return 0;
+    if (ctx)
+        if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipHostFree(ptr));
     return 0;
 }
 
@@ -967,10 +1056,13 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
         return 0;
     }
     if (int rc = set_device(ctx)) return rc;
+    units_per_batch = std::min(units_per_batch, ((batch->n_units + C - 1) / C) * C);
+    EncState* es = nullptr;
+    if (int rc = enc_state(ctx, units_per_batch / C, &es)) return rc;
     /* the caller's rows and output, page-locked in place for the call */
     const auto r0 = std::chrono::steady_clock::now();
     const size_t in_bytes = (size_t)((batch->n_units - 1) * batch->unit_stride + batch->block_len) * batch->sample_bytes;
-    /* a buffer already page-locked (flacmi_host_register, hipHostMalloc) is used as it is */
+    /* a buffer already page-locked (flacmi_host_register, flacmi_host_alloc) is used as it is */
     auto locked = [](const void* q) {
         hipPointerAttribute_t at{};
         const bool y = hipPointerGetAttributes(&at, q) == hipSuccess && at.type == hipMemoryTypeHost;
@@ -983,46 +1075,10 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
                          hipHostRegister(out, (size_t)out_capacity, hipHostRegisterDefault) == hipSuccess;
     (void)hipGetLastError();
     t.register_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
-    constexpr int kEncSlots = 3;
-    hipStream_t cs = nullptr, is = nullptr, os = nullptr;
-    EncSlot slot[kEncSlots];
+    hipStream_t cs = es->cs, is = es->is, os = es->os;
+    EncSlot* slot = es->slot;
     int rc = 0;
-    auto cleanup = [&]() {
-        for (hipStream_t st : {cs, is, os})
-            if (st) (void)hipStreamSynchronize(st);
-        for (auto& sl : slot) {
-            for (DevBuf* d : {&sl.samples, &sl.meta, &sl.params, &sl.residual, &sl.offsets, &sl.status, &sl.frames})
-                if (d->p) (void)hipFree(d->p);
-            if (sl.h_off) (void)hipHostFree(sl.h_off);
-            if (sl.h_st) (void)hipHostFree(sl.h_st);
-            for (auto& e : sl.e)
-                if (e) (void)hipEventDestroy(e);
-        }
-        for (hipStream_t st : {cs, is, os})
-            if (st) (void)hipStreamDestroy(st);
-        const auto u0 = std::chrono::steady_clock::now();
-        if (reg_in) (void)hipHostUnregister(const_cast<void*>(batch->samples));
-        if (reg_out) (void)hipHostUnregister(out);
-        t.register_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
-    };
-#define ENC_TRY(x)                                                                        \
-    do {                                                                                  \
-        hipError_t e_ = (x);                                                              \
-        if (e_ != hipSuccess) {                                                           \
-            rc = fail(FLACMI_E_HIP, "%s: %s", #x, hipGetErrorString(e_));                 \
-            goto done;                                                                    \
-        }                                                                                 \
-    } while (0)
     {
-        ENC_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-        ENC_TRY(hipStreamCreateWithFlags(&is, hipStreamNonBlocking));
-        ENC_TRY(hipStreamCreateWithFlags(&os, hipStreamNonBlocking));
-        const int64_t per_nf = units_per_batch / C;
-        for (auto& sl : slot) {
-            ENC_TRY(hipHostMalloc((void**)&sl.h_off, sizeof(int64_t) * (per_nf + 1), hipHostMallocDefault));
-            ENC_TRY(hipHostMalloc((void**)&sl.h_st, sizeof(int32_t) * per_nf, hipHostMallocDefault));
-            for (auto& e : sl.e) ENC_TRY(hipEventCreate(&e));
-        }
         const int64_t nsub = (batch->n_units + units_per_batch - 1) / units_per_batch;
         auto setup = [&](int64_t k) {
             EncSlot& sl = slot[k % kEncSlots];
@@ -1043,7 +1099,7 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
                 if ((sl.h_st[f] & 0xffff) == FLACMI_STATUS_RESIDUAL_WIDE) wide = true;
             if (wide) { /* a chosen residual needs 64 bits: redo this sub-batch with 8-byte rows */
                 sl.rbytes = 8;
-                if (int r = enc_front(ctx, sl, batch, params, fp, cs, is, os)) return r;
+                if (int r = enc_front(ctx, sl, batch, params, fp, cs, is)) return r;
                 HIP_TRY(hipEventSynchronize(sl.e[8]));
             }
             sl.total = sl.h_off[sl.nf];
@@ -1057,11 +1113,10 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
                             (long long)out_capacity);
             if (int r = ensure_buf(sl.frames, (size_t)sl.total + 16)) return r;
             const int64_t pstride = (1LL << (params->rice_max > 0 ? params->rice_max : 0)) + 1;
-            const int64_t sstride = ((sl.b.block_len * sl.b.sample_bytes + 15) / 16) * 16 / sl.b.sample_bytes;
             const int64_t rstride = ((sl.b.block_len * sl.rbytes + 15) / 16) * 16 / sl.rbytes;
             flacmi_batch db = sl.b;
             db.samples = sl.samples.p;
-            db.unit_stride = sstride;
+            db.unit_stride = sl.dstride;
             flacmi_frame_params f = *fp;
             f.first_frame = fp->first_frame + f0;
             FrameArgs a = frame_args(ctx, &db, &f, (const flacmi_unit_meta*)sl.meta.p, (const int32_t*)sl.params.p,
@@ -1099,16 +1154,24 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
         for (int64_t k = 0; k < nsub; ++k) {
             if (k >= kEncSlots) account(k - kEncSlots); /* the slot is free once those frames are copied */
             setup(k);
-            if ((rc = enc_front(ctx, slot[k % kEncSlots], batch, params, fp, cs, is, os))) goto done;
-            if (k >= 1 && (rc = back(k - 1))) goto done;
+            if ((rc = enc_front(ctx, slot[k % kEncSlots], batch, params, fp, cs, is))) break;
+            if (k >= 1 && (rc = back(k - 1))) break;
         }
-        if ((rc = back(nsub - 1))) goto done;
-        for (int64_t k = (nsub >= kEncSlots ? nsub - kEncSlots : 0); k < nsub; ++k) account(k);
+        if (!rc && (rc = back(nsub - 1)) == 0)
+            for (int64_t k = (nsub >= kEncSlots ? nsub - kEncSlots : 0); k < nsub; ++k) account(k);
         t.sub_batches = nsub;
     }
-done:
-#undef ENC_TRY
-    cleanup();
+    /* nothing may still read the caller's rows or write its buffer once this returns */
+    for (hipStream_t st : {cs, is, os}) {
+        hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess && !rc) rc = fail(FLACMI_E_HIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+    }
+    {
+        const auto u0 = std::chrono::steady_clock::now();
+        if (reg_in) (void)hipHostUnregister(const_cast<void*>(batch->samples));
+        if (reg_out) (void)hipHostUnregister(out);
+        t.register_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
+    }
     t.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     if (timing) *timing = t;
     return rc;

@@ -541,11 +541,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
 #pragma unroll 1
                 for (int t = 1;; ++t) {
                     const uint64_t lb = tj > (uint64_t)n ? tj - (uint64_t)n : 0ull;
-                    pruned = __ballot(lane >= 16 && lane < 16 + L && lb <= fmin) == 0;
+                    const uint64_t open = __ballot(lane >= 16 && lane < 16 + L && lb <= fmin);
+                    pruned = open == 0;
                     if (pruned || t == 4) break;
-                    /* the next quarter of the blocks (k % 4 == 2, 1, 3; block 0 is in tier 0) */
+                    /* the next quarter of the blocks (k % 4 == 2, 1, 3; block 0 is in tier 0), only
+                     * for the groups that hold an undecided order (mostly order 1's) */
+                    const uint32_t gneed = (uint32_t)(open >> 16);
                     __syncthreads(); /* every wave has read the bounds */
-                    for (int k = t == 1 ? 2 : t == 2 ? 1 : 3; k < kw; k += 4) block(I1{}, ING{}, I0{}, ld(wid + k * nw), false);
+                    for (int k = t == 1 ? 2 : t == 2 ? 1 : 3; k < kw; k += 4) {
+                        const h8 A = a_frag(ld(wid + k * nw));
+#pragma unroll
+                        for (int g = 1; g <= NG; ++g) {
+                            if ((gneed >> (4 * (g - 1))) & 15u) {
+                                const f4 D = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[g], C, 0, 0, 0);
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) acc[g] = opaque(sad32(__float_as_uint(D[r]), mbv, acc[g]));
+                            }
+                        }
+                    }
                     reduce_store(I1{}, I1{});
                     __syncthreads();
                     tj = lane_total();

@@ -10,8 +10,11 @@ the reference's exception at the same point of the stream.
 `encode_subframe_fixed`, `encode_subframe_lpc` and `encode_residual` are the
 single-unit forms of the same device analysis, returning the reference's dataclasses.
 """
+import collections
+import concurrent.futures
+import functools
 from dataclasses import dataclass
-from typing import Iterator, Optional
+from typing import Iterator, Optional, Sequence
 
 import numpy as np
 
@@ -105,8 +108,9 @@ def _sample_bits(a: np.ndarray) -> int:
     return max(2, m.bit_length() + 1)
 
 
-def _planar(blocks, channels: int, block_len: int):
-    """List of blocks (lists of frames) -> int16/int32 [n_blocks*channels][stride] rows."""
+def _planar(blocks, channels: int, block_len: int, alloc=None):
+    """List of blocks (lists of frames) -> int16/int32 [n_blocks*channels][stride] rows
+    (in alloc(shape, dtype)'s memory when given)."""
     nb = len(blocks)
     tail_len = len(blocks[-1])
     rows = np.zeros((nb * channels, block_len), dtype=np.int64)
@@ -116,7 +120,11 @@ def _planar(blocks, channels: int, block_len: int):
     bits = _sample_bits(rows)
     dt = np.int16 if bits <= 16 else np.int32
     stride = ((block_len * np.dtype(dt).itemsize + 15) // 16) * 16 // np.dtype(dt).itemsize
-    out = np.zeros((nb * channels, stride), dtype=dt)
+    if alloc is None:
+        out = np.zeros((nb * channels, stride), dtype=dt)
+    else:
+        out = alloc((nb * channels, stride), dt)
+        out[:, block_len:] = 0
     out[:, :block_len] = rows
     n_tail = channels if tail_len != block_len else 0
     return out, bits, tail_len, n_tail
@@ -176,90 +184,87 @@ def put_frame_header(header: FrameHeader) -> Put:
 
 def encode(sample_rate: int, sample_size: int, channels: int, frames: int,
            samples: Iterator[list], parameters: EncoderParameters, *, device: int = 0,
-           blocks_per_batch: int = 2048, fixed_only: bool = False) -> Iterator[bytes]:
+           devices: Optional[Sequence[int]] = None, blocks_per_batch: int = 2048,
+           fixed_only: bool = False) -> Iterator[bytes]:
     """flac/encoder.py:48-165 on the GPU: the per-channel analysis (k_lpc, k_resid) and
-    the frame writer (k_frame.hip: Rice packing, headers, CRC-8/16).  Only the stream
-    header (magic + STREAMINFO) is written here.
+    the frame writer (k_frame.hip: Rice packing, headers, CRC-8/16), streamed through
+    flacmi_encode_pipeline.  Only the stream header (magic + STREAMINFO) is written here.
 
-    fixed_only=True selects fixed predictors only (BASELINE config 5); the reference
-    has no such mode (its -l 0 raises ValueError, which the default mode reproduces)."""
+    devices: encode on several devices (or several contexts of one device: [0, 0]); the
+    batches go round-robin to one worker per entry and the frames come back in block
+    order, byte-identical to one device.  fixed_only=True selects fixed predictors only
+    (BASELINE config 5); the reference has no such mode (its -l 0 raises ValueError, which
+    the default mode reproduces)."""
     if sample_rate <= 48_000:
         assert parameters.lpc_order.stop <= 13
     yield from _stream_header(sample_rate, sample_size, channels, frames, parameters)
-    rmin, rmax = _rice_range(parameters.rice_partition_order)
-    L = parameters.lpc_order.stop - 1
-    mode = abi.MODE_FIXED_ONLY if fixed_only else abi.MODE_REFERENCE
-    params = make_params(L, parameters.qlp_precision, rmin, rmax, mode)
-    az = _analyzer(device)
-    index = 0
-    blocks_iter = batch(samples, parameters.block_size)
-    pending = []
-    for blk in blocks_iter:
-        pending.append(blk)
-        if len(pending) < blocks_per_batch:
-            continue
-        yield from _encode_batch(az, pending, index, channels, sample_size, parameters, params)
-        index += len(pending)
+    params = _params(parameters, fixed_only)
+    n = parameters.block_size
+
+    def batches():
+        index = 0
         pending = []
-    if pending:
-        yield from _encode_batch(az, pending, index, channels, sample_size, parameters, params)
+        for blk in batch(samples, n):
+            pending.append(blk)
+            if len(pending) == blocks_per_batch:
+                yield index, functools.partial(_planar, pending, channels, n)
+                index += len(pending)
+                pending = []
+        if pending:
+            yield index, functools.partial(_planar, pending, channels, n)
+
+    yield from _drive(batches(), _sessions(device, devices), params, n, channels, sample_size)
 
 
 def encode_planar(sample_rate: int, sample_size: int, pcm: np.ndarray, parameters: EncoderParameters, *,
-                  frames: Optional[int] = None, device: int = 0, blocks_per_batch: int = 8192,
-                  fixed_only: bool = False) -> Iterator[bytes]:
+                  frames: Optional[int] = None, device: int = 0, devices: Optional[Sequence[int]] = None,
+                  blocks_per_batch: int = 0, fixed_only: bool = False) -> Iterator[bytes]:
     """encode() over planar PCM (int [channels][frames], e.g. from ingest.read_wav): the
     same bytes as encode(sample_rate, sample_size, channels, frames, <the frames of pcm>,
-    parameters), without building a Python list per frame.  Blocks go to the device in
-    batches of blocks_per_batch (ingest.planar_blocks)."""
+    parameters), without building a Python list per frame.  Blocks are cut straight into
+    page-locked staging rows (ingest.planar_blocks) in batches of blocks_per_batch (0: about
+    256 MB of samples) and streamed through flacmi_encode_pipeline; devices as encode()."""
     from .ingest import planar_blocks
     channels, total = pcm.shape
     if sample_rate <= 48_000:
         assert parameters.lpc_order.stop <= 13
     yield from _stream_header(sample_rate, sample_size, channels, total if frames is None else frames,
                               parameters)
-    rmin, rmax = _rice_range(parameters.rice_partition_order)
-    mode = abi.MODE_FIXED_ONLY if fixed_only else abi.MODE_REFERENCE
-    params = make_params(parameters.lpc_order.stop - 1, parameters.qlp_precision, rmin, rmax, mode)
-    az = _analyzer(device)
+    params = _params(parameters, fixed_only)
     n = parameters.block_size
     nb = (total + n - 1) // n
-    for b0 in range(0, nb, blocks_per_batch):
-        rows, bits, tail_len, n_tail = planar_blocks(pcm, n, b0, blocks_per_batch)
-        data, offsets, status = az.encode_frames(rows, params, n, tail_len, n_tail, sample_bits=bits,
-                                                 channels=channels, sample_size=sample_size, first_frame=b0)
-        buf = data.tobytes()
-        for b in range(rows.shape[0] // channels):
-            st = int(status[b])
-            _raise_status(st & 0xFFFF, st >> 16)
-            yield buf[int(offsets[b]):int(offsets[b + 1])]
+    bpb = blocks_per_batch or _default_blocks(n, channels)
+
+    def batches():
+        for b0 in range(0, nb, bpb):
+            yield b0, functools.partial(planar_blocks, pcm, n, b0, bpb)
+
+    yield from _drive(batches(), _sessions(device, devices), params, n, channels, sample_size)
 
 
 def encode_wav(path, parameters: EncoderParameters, *, quirk: bool = True, device: int = 0,
-               blocks_per_batch: int = 8192, fixed_only: bool = False) -> Iterator[bytes]:
+               devices: Optional[Sequence[int]] = None, blocks_per_batch: int = 0,
+               fixed_only: bool = False) -> Iterator[bytes]:
     """The reference CLI's encode action (flac/__main__.py:58-109) on a WAV file, streamed:
-    the stream header first, then frames batch by batch (ingest.iter_wav_batches), so the
-    host holds one batch of PCM at a time.  A reader failure (the reference's IndexError on
-    its byte grouping, encoder.py:102) is raised after the stream header, as the reference
-    CLI has written it by then."""
-    from .ingest import iter_wav_batches, wav_info
+    the stream header first, then frames batch by batch (ingest.iter_wav_pcm), so the host
+    holds a bounded number of batches of PCM.  A reader failure (the reference's IndexError
+    on its byte grouping, encoder.py:102) is raised after the stream header and the frames
+    of the batches before it, as the reference CLI has written them by then."""
+    from .ingest import iter_wav_pcm, planar_blocks, wav_info
     info = wav_info(path)
     if info.sample_rate <= 48_000:
         assert parameters.lpc_order.stop <= 13
     yield from _stream_header(info.sample_rate, info.sample_width * 8, info.channels, info.frames, parameters)
-    rmin, rmax = _rice_range(parameters.rice_partition_order)
-    mode = abi.MODE_FIXED_ONLY if fixed_only else abi.MODE_REFERENCE
-    params = make_params(parameters.lpc_order.stop - 1, parameters.qlp_precision, rmin, rmax, mode)
+    params = _params(parameters, fixed_only)
     n, C = parameters.block_size, info.channels
-    for b0, rows, bits, tail_len, n_tail in iter_wav_batches(path, n, blocks_per_batch, quirk):
-        az = _analyzer(device)  # after the first batch is read: a reader failure needs no device
-        data, offsets, status = az.encode_frames(rows, params, n, tail_len, n_tail, sample_bits=bits,
-                                                 channels=C, sample_size=info.sample_width * 8, first_frame=b0)
-        buf = data.tobytes()
-        for b in range(rows.shape[0] // C):
-            st = int(status[b])
-            _raise_status(st & 0xFFFF, st >> 16)
-            yield buf[int(offsets[b]):int(offsets[b + 1])]
+    bpb = blocks_per_batch or _default_blocks(n, C)
+
+    def batches():
+        for b0, pcm in iter_wav_pcm(path, n, bpb, quirk):
+            yield b0, functools.partial(planar_blocks, pcm, n)
+
+    # sessions are opened after the first batch is read: a reader failure needs no device
+    yield from _drive(batches(), lambda: _sessions(device, devices), params, n, C, info.sample_width * 8)
 
 
 def _stream_header(sample_rate, sample_size, channels, frames, parameters):
@@ -272,13 +277,121 @@ def _stream_header(sample_rate, sample_size, channels, frames, parameters):
         sample_size=sample_size, samples=frames, md5=bytes(16))).buffer
 
 
-def _encode_batch(az, blocks, index0, channels, sample_size, parameters, params):
-    n = parameters.block_size
-    rows, bits, tail_len, n_tail = _planar(blocks, channels, n)
-    data, offsets, status = az.encode_frames(rows, params, n, tail_len, n_tail, sample_bits=bits,
-                                             channels=channels, sample_size=sample_size, first_frame=index0)
-    buf = data.tobytes()
-    for b in range(len(blocks)):
+def _params(parameters: EncoderParameters, fixed_only: bool) -> abi.Params:
+    rmin, rmax = _rice_range(parameters.rice_partition_order)
+    mode = abi.MODE_FIXED_ONLY if fixed_only else abi.MODE_REFERENCE
+    return make_params(parameters.lpc_order.stop - 1, parameters.qlp_precision, rmin, rmax, mode)
+
+
+# ---------------------------------------------------------------------------------
+# streaming driver: page-locked staging, flacmi_encode_pipeline, one worker per device
+# ---------------------------------------------------------------------------------
+_BATCH_BYTES = 256 << 20   # samples per batch (about): one pipeline call's worth of PCM
+_SUB_UNITS = 8192          # units per pipeline sub-batch (the copies of one overlap the others' kernels)
+
+
+def _default_blocks(block_size: int, channels: int) -> int:
+    return max(1, _BATCH_BYTES // (4 * max(block_size, 1) * max(channels, 1)))
+
+
+class _Session:
+    """One encode context (one flacmi_ctx on `device`): two page-locked staging buffers
+    for sample rows (the host cuts batch k + 1 into one while the device encodes batch k
+    from the other), a page-locked frame buffer and one worker thread, all reused batch
+    after batch."""
+
+    def __init__(self, device: int):
+        self.az = Analyzer(device)
+        self.stage = [None, None]
+        self.out = None
+        self.pool = concurrent.futures.ThreadPoolExecutor(1)
+
+    def staging(self, slot: int, shape, dtype) -> np.ndarray:
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        buf = self.stage[slot]
+        if buf is None or buf.size < nbytes:
+            buf = self.stage[slot] = self.az.host_array((max(nbytes, 1),), np.uint8)
+        return buf[:nbytes].view(dtype).reshape(shape)
+
+    def encode(self, rows, bits, tail_len, n_tail, params, n, channels, sample_size, first_frame):
+        """-> (frame bytes, offsets, status) of one batch (host copies: the buffers are reused)."""
+        cap = int(rows.shape[0] * (n * rows.itemsize * 1.25 + 256)) + (1 << 20)
+        while True:
+            if self.out is None or self.out.size < cap:
+                self.out = None
+                self.out = self.az.host_array((cap,), np.uint8)
+            try:
+                data, offsets, status, _ = self.az.encode_pipeline(
+                    rows, params, n, tail_len, n_tail, sample_bits=bits, channels=channels,
+                    sample_size=sample_size, first_frame=first_frame, units_per_batch=_SUB_UNITS,
+                    out=self.out)
+            except FlacmiError as e:
+                if e.code == abi.E_NOMEM:
+                    cap = 2 * max(cap, self.out.size)
+                    continue
+                raise
+            return data.tobytes(), offsets, status
+
+
+_SESSIONS = {}
+
+
+def _sessions(device: int, devices: Optional[Sequence[int]]):
+    """One cached session per entry of devices (an entry repeated: another context on that
+    device)."""
+    out = []
+    seen = {}
+    for d in (list(devices) if devices else [device]):
+        k = (int(d), seen.get(int(d), 0))
+        seen[int(d)] = k[1] + 1
+        if k not in _SESSIONS:
+            _SESSIONS[k] = _Session(int(d))
+        out.append(_SESSIONS[k])
+    if not out:
+        raise ValueError("devices is empty")
+    return out
+
+
+def _drive(batches, sessions, params, n, channels, sample_size) -> Iterator[bytes]:
+    """batches yields (first_block, cut) with cut(alloc=...) -> (rows, bits, tail_len,
+    n_tail_units); batch i goes to sessions[i % D].  Frames are yielded in block order; a
+    frame the reference would fail on raises its exception after the frames before it, and
+    an exception from `batches` itself (the WAV reader) after every earlier batch's frames."""
+    queue = collections.deque()
+    failure = None
+    it = iter(batches)
+    i = 0
+    while True:
+        try:
+            item = next(it)
+        except StopIteration:
+            break
+        except Exception as e:  # the reader's failure surfaces in stream order
+            failure = e
+            break
+        if callable(sessions):
+            sessions = sessions()
+        D = len(sessions)
+        while len(queue) >= 2 * D:  # batch i reuses the staging slot of batch i - 2D
+            yield from _frames(*queue.popleft().result())
+        first_block, cut = item
+        s, slot = sessions[i % D], (i // D) % 2
+        try:
+            rows, bits, tail_len, n_tail = cut(alloc=functools.partial(s.staging, slot))
+        except Exception as e:
+            failure = e
+            break
+        queue.append(s.pool.submit(s.encode, rows, bits, tail_len, n_tail, params, n, channels, sample_size,
+                                   first_block))
+        i += 1
+    while queue:
+        yield from _frames(*queue.popleft().result())
+    if failure is not None:
+        raise failure
+
+
+def _frames(buf: bytes, offsets: np.ndarray, status: np.ndarray) -> Iterator[bytes]:
+    for b in range(len(status)):
         st = int(status[b])
         _raise_status(st & 0xFFFF, st >> 16)  # the reference raises after the frames before it
         yield buf[int(offsets[b]):int(offsets[b + 1])]

@@ -62,6 +62,22 @@ def wav_info(path) -> PcmInfo:
         return PcmInfo(w.getframerate(), w.getsampwidth(), w.getnchannels(), w.getnframes())
 
 
+def iter_wav_pcm(path, block_size: int, blocks_per_batch: int, quirk: bool = True):
+    """Stream a WAV file as int64 [channels][frames] pieces of blocks_per_batch * block_size
+    frames: yields (first_block, pcm), so memory is bounded by one batch whatever the file
+    size.  planar_blocks(pcm, block_size) cuts a piece into device rows."""
+    with wave.open(str(path), "rb") as w:
+        channels, width = w.getnchannels(), w.getsampwidth()
+        first = 0
+        while True:
+            raw = w.readframes(blocks_per_batch * block_size)
+            if not raw:
+                return
+            pcm = frames_to_channels(raw, channels, width, quirk)
+            yield first, pcm
+            first += (pcm.shape[1] + block_size - 1) // block_size
+
+
 def iter_wav_batches(path, block_size: int, blocks_per_batch: int, quirk: bool = True):
     """Stream a WAV file as device-ready batches: yields (first_block, rows, bits, tail_len,
     n_tail_units) exactly as planar_blocks() cuts them, reading blocks_per_batch *
@@ -102,11 +118,12 @@ def sample_bits(pcm: np.ndarray) -> int:
     return max(2, m.bit_length() + 1)
 
 
-def planar_blocks(pcm: np.ndarray, block_size: int, first_block: int = 0, n_blocks: int = -1):
+def planar_blocks(pcm: np.ndarray, block_size: int, first_block: int = 0, n_blocks: int = -1, alloc=None):
     """int64 [channels][frames] -> (rows [n_blocks*channels][stride] int16/int32, bits,
     tail_len, n_tail_units) for blocks [first_block, first_block + n_blocks) of
     utils.batch(frames, block_size).  Rows are 16-byte aligned; samples past a short
-    block's end are zero."""
+    block's end are zero.  alloc(shape, dtype) (optional) supplies the rows' memory, e.g.
+    a page-locked staging buffer reused batch after batch."""
     C, frames = pcm.shape
     total = (frames + block_size - 1) // block_size
     if n_blocks < 0:
@@ -119,12 +136,17 @@ def planar_blocks(pcm: np.ndarray, block_size: int, first_block: int = 0, n_bloc
     dt = np.int16 if bits <= 16 else np.int32
     isz = np.dtype(dt).itemsize
     stride = ((block_size * isz + 15) // 16) * 16 // isz
-    rows = np.zeros((n_blocks, C, stride), dtype=dt)
+    if alloc is None:
+        rows = np.zeros((n_blocks, C, stride), dtype=dt)
+    else:
+        rows = alloc((n_blocks, C, stride), dt)
+        rows[:, :, block_size:] = 0
     full = seg.shape[1] // block_size
     if full:
         rows[:full, :, :block_size] = seg[:, :full * block_size].reshape(C, full, block_size).transpose(1, 0, 2)
     tail_len = seg.shape[1] - full * block_size
     if tail_len:
         rows[full, :, :tail_len] = seg[:, full * block_size:]
+        rows[full, :, tail_len:] = 0
     n_tail = C if tail_len else 0
     return rows.reshape(n_blocks * C, stride), bits, (tail_len if tail_len else block_size), n_tail

@@ -292,6 +292,14 @@ int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch, const fla
 int flacmi_host_register(flacmi_ctx* ctx, void* ptr, size_t bytes);
 int flacmi_host_unregister(flacmi_ctx* ctx, void* ptr);
 
+/* Page-locked host memory owned by the caller until flacmi_host_free (hipHostMalloc on the
+ * context's device): the staging rows and frame buffer a streaming caller fills and drains
+ * batch after batch (flac_amd.encoder's encode paths), with no per-call page-locking.
+ * NULL (flacmi_last_error) if it cannot be allocated.  flacmi_host_free takes a NULL ctx too
+ * (memory that outlives its context). */
+void* flacmi_host_alloc(flacmi_ctx* ctx, size_t bytes);
+int flacmi_host_free(flacmi_ctx* ctx, void* ptr);
+
 /* ---- decoder verifier (BASELINE config 5 round trip) ------------- */
 /* Replaces the reference's frame decoder: decoder.py:111-130 get_frame, :133-190
  * get_frame_header (+ coded_number.py:45-70 decode), :192-245 field decoders, :267-344

@@ -142,3 +142,35 @@ def test_encode_residual(enc, synth, nm, i):
     for q in r.partitions:
         h.update(b"".join(int(x).to_bytes(8, "little") for x in q.residual))
     assert h.hexdigest() == exp["zz_sha256"]
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_stream_c1_multi_context_matches_reference(enc, devices):
+    """encode(devices=[...]): batches round-robin over several contexts (two or three on
+    one GPU here), frames merged in block order: byte-identical to the reference."""
+    S = G.load("streams.json")
+    pcm = _sine(441000)
+    p = enc.EncoderParameters(block_size=4608, rice_partition_order=range(0, 6),
+                              lpc_order=range(0, 9), qlp_precision=5)
+    for bpb in (1, 5):
+        assert _stream(enc, 44100, 16, 1, len(pcm), [pcm], p, blocks_per_batch=bpb, devices=devices) == \
+            (S["c1_correct"]["len"], S["c1_correct"]["sha256"])
+
+
+def test_encode_planar_multi_context_and_frame_error_order(enc):
+    """encode_planar over two contexts equals one context; a unit the reference fails on
+    (an all-zero block: ZeroDivisionError in levinson_durbin) raises after exactly the
+    frames before it, whichever context encoded its batch."""
+    pcm = np.array([_sine(4608 * 9)], dtype=np.int64)
+    p = enc.EncoderParameters(block_size=4608, rice_partition_order=range(0, 6),
+                              lpc_order=range(0, 13), qlp_precision=5)
+    one = list(enc.encode_planar(44100, 16, pcm, p, blocks_per_batch=2))
+    two = list(enc.encode_planar(44100, 16, pcm, p, blocks_per_batch=2, devices=[0, 0]))
+    assert one == two and len(one) == 3 + 9
+    bad = pcm.copy()
+    bad[0, 4608 * 5:4608 * 6] = 0
+    got = []
+    with pytest.raises(ZeroDivisionError):
+        for f in enc.encode_planar(44100, 16, bad, p, blocks_per_batch=2, devices=[0, 0]):
+            got.append(f)
+    assert got == one[:3 + 5]
