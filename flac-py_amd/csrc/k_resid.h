@@ -564,12 +564,19 @@ __device__ __forceinline__ void mf8_tile_epilogue(const v4i (&D)[4], int s, cons
 
 /* Sums of |r| for LPC orders 1..L (into red[wid][5 + p - 1]) and fixed orders 0..4 (VALU,
  * 8-sample chunks, into red[wid][0..4]).  pl: the three digit planes, PLB bytes apart;
- * cfl / lsh: phase A's coefficient and shift tables; G: tiles per u32 partial sum. */
+ * cfl / lsh: phase A's coefficient and shift tables; G: tiles per u32 partial sum.
+ *
+ * prune (reference mode): the tiles run in four tiers, the wave's tiles k % 4 == 0, then
+ * 2, 1, 3.  After each tier every wave reads the workgroup's exact partial LPC sums (a sum
+ * over a subset of the values, so a lower bound of each order's full sum) against the best
+ * exact fixed sum; once every order's partial sum exceeds it, LPC can neither win nor tie
+ * (encoder.py:135-157) and the remaining tiers are skipped: returns true (workgroup-uniform;
+ * red then holds partial LPC sums).  Otherwise the four tiers add up to the exact sums. */
 template <int LMAX>
-__device__ __forceinline__ void mf8_candidate_sums(const int32_t* xs32, const unsigned char* pl, int PLB,
+__device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const unsigned char* pl, int PLB,
                                                    const int32_t* cfl, const int32_t* lsh, int L, int n, int G,
                                                    int tid, int NT, int lane, int wid, int nw,
-                                                   unsigned long long* red) {
+                                                   unsigned long long* red, bool prune) {
     using CT = CoefTables<LMAX>;
     constexpr int NSUM = 5 + LMAX;
     constexpr int NTMAX = (LMAX + 15) / 16;
@@ -678,9 +685,8 @@ __device__ __forceinline__ void mf8_candidate_sums(const int32_t* xs32, const un
      * epilogue of tile T, the matrix cores run the MFMAs of the next tile and the LDS
      * delivers the windows of the one after (clamped index: no guarded loads; a clamped
      * tile's MFMAs are never used). */
-    auto run = [&](auto NTL_) __attribute__((always_inline)) {
+    auto run = [&](auto NTL_, int T, const int step) __attribute__((always_inline)) {
         constexpr int NTL = decltype(NTL_)::value;
-        int T = wid;
         Mf8Raw a0, a1, a2, b0, b1, b2;
         v4i DA[NTL][4], DB[NTL][4];
         while (T < 2 && T < ntile) {
@@ -689,7 +695,7 @@ __device__ __forceinline__ void mf8_candidate_sums(const int32_t* xs32, const un
             mf8_load(pw2 + 4 * T, a2);
             mm(a0, a1, a2, DA);
             ep(DA, T, std::true_type{});
-            T += nw;
+            T += step;
         }
         flush();
         if (T >= ntile) return;
@@ -697,49 +703,82 @@ __device__ __forceinline__ void mf8_candidate_sums(const int32_t* xs32, const un
         mf8_load(pw1 + 4 * T, a1);
         mf8_load(pw2 + 4 * T, a2);
         mm(a0, a1, a2, DA);
-        int Tn = T + nw < ntile ? T + nw : T;
+        int Tn = T + step < ntile ? T + step : T;
         mf8_load(pw0 + 4 * Tn, b0);
         mf8_load(pw1 + 4 * Tn, b1);
         mf8_load(pw2 + 4 * Tn, b2);
         int g = 0;
         for (;;) {
-            int Tnn = Tn + nw < ntile ? Tn + nw : Tn;
+            int Tnn = Tn + step < ntile ? Tn + step : Tn;
             mm(b0, b1, b2, DB);
             mf8_load(pw0 + 4 * Tnn, a0);
             mf8_load(pw1 + 4 * Tnn, a1);
             mf8_load(pw2 + 4 * Tnn, a2);
             ep(DA, T, std::false_type{});
-            T += nw;
+            T += step;
             if (++g == G) flush(), g = 0;
             if (T >= ntile) break;
             Tn = Tnn;
-            Tnn = Tn + nw < ntile ? Tn + nw : Tn;
+            Tnn = Tn + step < ntile ? Tn + step : Tn;
             mm(a0, a1, a2, DA);
             mf8_load(pw0 + 4 * Tnn, b0);
             mf8_load(pw1 + 4 * Tnn, b1);
             mf8_load(pw2 + 4 * Tnn, b2);
             ep(DB, T, std::false_type{});
-            T += nw;
+            T += step;
             if (++g == G) flush(), g = 0;
             if (T >= ntile) break;
             Tn = Tnn;
         }
         flush();
     };
-    if constexpr (NTMAX >= 2) {
-        if (L > 16) run(std::integral_constant<int, 2>{});
-        else run(std::integral_constant<int, 1>{});
-    } else {
-        run(std::integral_constant<int, 1>{});
-    }
+    /* tiles T0, T0 + step, ... (the first two tiles, samples < 32 >= every start, masked) */
+    auto go = [&](int T0, int step) __attribute__((always_inline)) {
+        if constexpr (NTMAX >= 2) {
+            if (L > 16) run(std::integral_constant<int, 2>{}, T0, step);
+            else run(std::integral_constant<int, 1>{}, T0, step);
+        } else {
+            run(std::integral_constant<int, 1>{}, T0, step);
+        }
+    };
+    /* this wave's running LPC sums (cumulative over tiers) into red */
+    auto store = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int nt = 0; nt < NTMAX; ++nt) {
-        uint64_t v = acc[nt];
-        v += (uint64_t)__shfl_xor((unsigned long long)v, 16);
-        v += (uint64_t)__shfl_xor((unsigned long long)v, 32);
-        const int p = 16 * nt + col + 1;
-        if (lane < 16 && p <= LMAX) red[wid * NSUM + 4 + p] = p <= L ? v : 0ull;
+        for (int nt = 0; nt < NTMAX; ++nt) {
+            uint64_t v = acc[nt];
+            v += (uint64_t)__shfl_xor((unsigned long long)v, 16);
+            v += (uint64_t)__shfl_xor((unsigned long long)v, 32);
+            const int p = 16 * nt + col + 1;
+            if (lane < 16 && p <= LMAX) red[wid * NSUM + 4 + p] = p <= L ? v : 0ull;
+        }
+    };
+    if (!prune) {
+        go(wid, nw);
+        store();
+        return false;
     }
+    bool pruned = false;
+#pragma unroll 1
+    for (int t = 0; t < 4; ++t) {
+        go(wid + (t == 0 ? 0 : t == 1 ? 2 : t == 2 ? 1 : 3) * nw, 4 * nw);
+        store();
+        if (t == 3) break; /* every tile done: the sums are exact */
+        __syncthreads();
+        uint64_t tj = 0;
+        if (lane < NSUM)
+            for (int w2 = 0; w2 < nw; ++w2) tj += red[w2 * NSUM + lane];
+        uint64_t fmin = ~0ull;
+#pragma unroll
+        for (int o = 0; o < 5; ++o) {
+            const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tj >> 32), o) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tj, o);
+            fmin = v < fmin ? v : fmin;
+        }
+        pruned = __ballot(lane >= 5 && lane < 5 + L && tj <= fmin) == 0;
+        __syncthreads(); /* every wave has read red before the next tier stores */
+        if (pruned) break;
+    }
+    return pruned;
 }
 
 /* Phase E of the fast kernel for a fixed predictor of order K (encoder.py:331-359,
@@ -1052,7 +1091,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
      * per-wave max|x| in the (unused) MFMA tap-table region */
     const int PLB = mf8_plane_bytes(n);
     uint32_t* mf8_xmax = reinterpret_cast<uint32_t*>(smem + lay.coef + CT::TAPF_OFF); /* [nw] */
-    bool use_mf8 = false;
+    bool use_mf8 = false, lpc_pruned = false;
     int mf8_G = 0;
     int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
     int32_t* xs32 = reinterpret_cast<int32_t*>(smem + lay.xs) + HP; /* [-HP, npad) (others) */
@@ -1402,7 +1441,8 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
         if (a.stop_after == 2) return;
     } else if (MF8 && use_mf8) {
         if constexpr (MF8)
-            mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid, nw, red);
+            lpc_pruned = mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
+                                                  nw, red, a.prune != 0 && !lpc_only && !rice_only);
         if (a.stop_after == 2) return;
     } else if constexpr (!FAST) {
     A acc[NSUM];
@@ -1491,7 +1531,10 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             fsum = 0;
             dorder = a.rice_order; /* identity "predictor": the row already is the residual */
         }
-        if (do_lpc) {
+        if (do_lpc && lpc_pruned) { /* every LPC candidate provably loses (mf8_candidate_sums) */
+            lbest = FLACMI_LPC_PRUNED;
+            lsum = (uint64_t)(int64_t)FLACMI_LPC_PRUNED;
+        } else if (do_lpc) {
             lbest = 1;
             lsum = tot_at(5);
             static_for<LMAX>([&](auto P_) {
