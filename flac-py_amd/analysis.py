@@ -266,9 +266,10 @@ class Analyzer:
         if not p:
             raise FlacmiError(f"flacmi_host_alloc({nbytes}): {self.lib.flacmi_last_error().decode(errors='replace')}")
         raw = (C.c_uint8 * nbytes).from_address(p)
-        a = np.frombuffer(raw, dtype=dt, count=count).reshape(shape)
-        weakref.finalize(a, self.lib.flacmi_host_free, None, p)  # valid after close() too
-        return a
+        # every numpy view of the memory keeps `raw` alive: free with the last view (valid
+        # after close() too)
+        weakref.finalize(raw, self.lib.flacmi_host_free, None, p)
+        return np.frombuffer(raw, dtype=dt, count=count).reshape(shape)
 
     def frame_sizes_device(self, batch: abi.Batch, fp: abi.FrameParams, meta_ptr: int, params_ptr: int,
                            params_stride: int, offsets_ptr: int, status_ptr: int, stream: int = 0) -> None:

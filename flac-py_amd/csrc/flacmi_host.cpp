@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -186,6 +187,7 @@ static int ensure_buf(DevBuf& b, size_t bytes) {
 }
 
 static int set_device(flacmi_ctx* ctx) {
+    if (!ctx) return fail(FLACMI_E_INVALID, "null context");
     HIP_TRY(hipSetDevice(ctx->device));
     return 0;
 }
@@ -868,8 +870,9 @@ int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_
 }
 
 /* ---- pipelined host encode ---------------------------------------------------------
- * Streams: `cs` (compute: analysis, sizes, the small offsets/status copy back, pack, in
- * order, so the context's shared scratch is never used by two launches at once), `is`
+ * Streams: `cs` = the context's stream (compute: analysis, sizes, the small offsets/status
+ * copy back, pack, in order, so the context's shared scratch is never used by two launches
+ * at once), `is`
  * (host -> device samples) and `os` (device -> host frame bytes).  Per sub-batch k (slot
  * k % kEncSlots):
  *   front(k): is: H2D rows -> cs: analyze, frame sizes, offsets/status D2H (pinned)
@@ -898,14 +901,14 @@ float ev_ms(hipEvent_t a, hipEvent_t b) {
 }  // namespace
 
 struct EncState {
-    hipStream_t cs = nullptr, is = nullptr, os = nullptr;
+    hipStream_t is = nullptr, os = nullptr; /* compute runs on the context's stream */
     EncSlot slot[kEncSlots];
     int64_t cap_nf = 0; /* frames the pinned arrays of each slot hold */
 };
 
 static void enc_free(EncState* es) {
     if (!es) return;
-    for (hipStream_t st : {es->cs, es->is, es->os})
+    for (hipStream_t st : {es->is, es->os})
         if (st) (void)hipStreamSynchronize(st);
     for (auto& sl : es->slot) {
         for (DevBuf* d : {&sl.samples, &sl.meta, &sl.params, &sl.residual, &sl.offsets, &sl.status, &sl.frames})
@@ -915,7 +918,7 @@ static void enc_free(EncState* es) {
         for (auto& e : sl.e)
             if (e) (void)hipEventDestroy(e);
     }
-    for (hipStream_t st : {es->cs, es->is, es->os})
+    for (hipStream_t st : {es->is, es->os})
         if (st) (void)hipStreamDestroy(st);
     delete es;
 }
@@ -924,7 +927,6 @@ static int enc_state(flacmi_ctx* ctx, int64_t per_nf, EncState** out) {
     if (!ctx->enc) {
         EncState* es = new EncState();
         ctx->enc = es;
-        HIP_TRY(hipStreamCreateWithFlags(&es->cs, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&es->is, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&es->os, hipStreamNonBlocking));
         for (auto& sl : es->slot)
@@ -1075,7 +1077,11 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
                          hipHostRegister(out, (size_t)out_capacity, hipHostRegisterDefault) == hipSuccess;
     (void)hipGetLastError();
     t.register_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r0).count();
-    hipStream_t cs = es->cs, is = es->is, os = es->os;
+    /* three streams in all (with the null stream four: GPU_MAX_HW_QUEUES' default).  With a
+     * fifth the runtime maps two streams onto one hardware queue, and the copies of the two
+     * directions then wait for each other in submission order (measured: H2D of sub-batch
+     * k + 2 started only when the D2H of k had finished). */
+    hipStream_t cs = ctx->stream, is = es->is, os = es->os;
     EncSlot* slot = es->slot;
     int rc = 0;
     {
@@ -1141,9 +1147,16 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
             t.bytes_out += sl.total;
             return 0;
         };
+        /* diagnostic (FLACMI_ENC_TRACE): per-sub-batch timeline in ms from the call's start */
+        hipEvent_t tb = nullptr;
+        if (std::getenv("FLACMI_ENC_TRACE") && hipEventCreate(&tb) == hipSuccess) (void)hipEventRecord(tb, is);
         auto account = [&](int64_t k) {
             EncSlot& sl = slot[k % kEncSlots];
             (void)hipEventSynchronize(sl.e[7]);
+            if (tb)
+                std::fprintf(stderr, "enc %lld: h2d %.2f-%.2f an-end %.2f sz-end %.2f off %.2f pack %.2f-%.2f d2h %.2f-%.2f\n",
+                             (long long)k, ev_ms(tb, sl.e[0]), ev_ms(tb, sl.e[1]), ev_ms(tb, sl.e[2]), ev_ms(tb, sl.e[3]),
+                             ev_ms(tb, sl.e[8]), ev_ms(tb, sl.e[4]), ev_ms(tb, sl.e[5]), ev_ms(tb, sl.e[6]), ev_ms(tb, sl.e[7]));
             t.h2d_ms += ev_ms(sl.e[0], sl.e[1]);
             t.analyze_ms += ev_ms(sl.e[1], sl.e[2]);
             t.sizes_ms += ev_ms(sl.e[2], sl.e[3]);
@@ -1160,6 +1173,7 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
         if (!rc && (rc = back(nsub - 1)) == 0)
             for (int64_t k = (nsub >= kEncSlots ? nsub - kEncSlots : 0); k < nsub; ++k) account(k);
         t.sub_batches = nsub;
+        if (tb) (void)hipEventDestroy(tb);
     }
     /* nothing may still read the caller's rows or write its buffer once this returns */
     for (hipStream_t st : {cs, is, os}) {
@@ -1300,6 +1314,7 @@ double flacmi_host_pypow2(double x, int32_t* status) {
 
 int32_t flacmi_host_floor_log2(double x) {
     ensure_tables();
+    if (!(x > 0.0) || std::isinf(x)) return INT32_MIN; /* outside the domain (the table covers finite x > 0) */
     return pym::py_floor_log2(x, g_log2thr.data());
 }
 

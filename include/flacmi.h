@@ -403,7 +403,7 @@ int flacmi_timing_reset(flacmi_ctx* ctx);
  * *status receives FLACMI_STATUS_OVERFLOW where Python raises OverflowError. */
 double flacmi_host_pypow2(double x, int32_t* status);
 /* floor(math.log2(x)) for finite x > 0, via the threshold table the device uses
- * (built once per process from libm log2). */
+ * (built once per process from libm log2); INT32_MIN for any other x. */
 int32_t flacmi_host_floor_log2(double x);
 
 /* The same helpers executed by the device kernels, over n host inputs (synchronous):
