@@ -870,25 +870,28 @@ int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_
 }
 
 /* ---- pipelined host encode ---------------------------------------------------------
- * Streams: `cs` = the context's stream (compute: analysis, sizes, the small offsets/status
- * copy back, pack, in order, so the context's shared scratch is never used by two launches
+ * Streams: `cs` = the context's stream (compute: analysis, sizes, k_export of the offsets /
+ * status into mapped host memory, pack, in order, so the context's shared scratch is never used by two launches
  * at once), `is`
  * (host -> device samples) and `os` (device -> host frame bytes).  Per sub-batch k (slot
  * k % kEncSlots):
- *   front(k): is: H2D rows -> cs: analyze, frame sizes, offsets/status D2H (pinned)
+ *   front(k): is: H2D rows -> cs: analyze, frame sizes, k_export (offsets/status to host)
  *   back(k):  host waits for those offsets, then cs: pack -> os: frame bytes D2H into out
  * issued as front(0), front(1), back(0), front(2), back(1), ... so the copies of one
- * sub-batch run under the kernels of the others.  The offsets of k ride the compute stream:
- * on `os` they would queue behind the frame bytes of k - 1 and the host would wait for that
- * copy before issuing the next H2D (the two copy directions then ran back to back).
+ * sub-batch run under the kernels of the others.  The offsets of k are written by a kernel
+ * into mapped host memory: as a DMA copy they queued behind the frame bytes of k - 1 and
+ * the host waited for that copy before issuing the next H2D (the two copy directions then
+ * ran back to back).
  * Streams, events, slot buffers and the pinned offset arrays live in the context and grow
  * as needed (ensure_buf), so streaming many calls pays no setup. */
 namespace {
-constexpr int kEncSlots = 3;
+constexpr int kEncSlots = 4; /* with 3 the host waited for the D2H of sub-batch k - 3 before issuing the H2D of k */
 struct EncSlot {
     DevBuf samples, meta, params, residual, offsets, status, frames;
-    int64_t* h_off = nullptr;   /* pinned: frame offsets of the sub-batch */
-    int32_t* h_st = nullptr;    /* pinned: frame status */
+    int64_t* h_off = nullptr;   /* pinned, mapped: frame offsets of the sub-batch */
+    int32_t* h_st = nullptr;    /* pinned, mapped: frame status */
+    int64_t* d_off = nullptr;   /* their device-side addresses (k_export writes them) */
+    int32_t* d_st = nullptr;
     hipEvent_t e[9] = {};       /* h2d start/end, analyze end, sizes end, pack start/end, d2h start/end, offsets copied */
     flacmi_batch b{};
     int64_t first_unit = 0, nf = 0, total = 0, dstride = 0;
@@ -942,8 +945,10 @@ static int enc_state(flacmi_ctx* ctx, int64_t per_nf, EncState** out) {
         }
         es->cap_nf = 0;
         for (auto& sl : es->slot) {
-            HIP_TRY(hipHostMalloc((void**)&sl.h_off, sizeof(int64_t) * (per_nf + 1), hipHostMallocDefault));
-            HIP_TRY(hipHostMalloc((void**)&sl.h_st, sizeof(int32_t) * per_nf, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&sl.h_off, sizeof(int64_t) * (per_nf + 1), hipHostMallocMapped | hipHostMallocCoherent));
+            HIP_TRY(hipHostMalloc((void**)&sl.h_st, sizeof(int32_t) * per_nf, hipHostMallocMapped | hipHostMallocCoherent));
+            HIP_TRY(hipHostGetDevicePointer((void**)&sl.d_off, sl.h_off, 0));
+            HIP_TRY(hipHostGetDevicePointer((void**)&sl.d_st, sl.h_st, 0));
         }
         es->cap_nf = per_nf;
     }
@@ -995,8 +1000,7 @@ static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, co
     FrameArgs a = frame_args(ctx, &db, &f, o.meta, o.rice_params, pstride, sl.nf);
     if (int rc = frame_sizes_impl(ctx, a, (int64_t*)sl.offsets.p, (int32_t*)sl.status.p, cs)) return rc;
     HIP_TRY(hipEventRecord(sl.e[3], cs));
-    HIP_TRY(hipMemcpyAsync(sl.h_off, sl.offsets.p, sizeof(int64_t) * (sl.nf + 1), hipMemcpyDeviceToHost, cs));
-    HIP_TRY(hipMemcpyAsync(sl.h_st, sl.status.p, sizeof(int32_t) * sl.nf, hipMemcpyDeviceToHost, cs));
+    HIP_TRY(launch_export((const int64_t*)sl.offsets.p, (const int32_t*)sl.status.p, sl.nf, sl.d_off, sl.d_st, cs));
     HIP_TRY(hipEventRecord(sl.e[8], cs));
     return 0;
 }

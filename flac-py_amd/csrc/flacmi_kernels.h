@@ -123,6 +123,9 @@ constexpr int kMaxFinestParts = 4096;
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);
 /* test knob: fill every CU's LDS with a pattern (env FLACMI_POISON_LDS), else nothing */
 hipError_t launch_poison_lds(hipStream_t s);
+/* copy nf + 1 frame offsets and nf statuses to mapped host memory (k_misc.hip) */
+hipError_t launch_export(const int64_t* off, const int32_t* st, int64_t nf, int64_t* h_off, int32_t* h_st,
+                         hipStream_t s);
 /* k_lpc<32> with the autocorrelation read from a.acf (flacmi_device_lpc_from_acf) */
 hipError_t launch_lpc_from_acf(const LpcArgs& a, hipStream_t s);
 /* path: 0 = int16 samples / sdot2, 1 = int32 samples / mad24, 2 = int64 arithmetic */

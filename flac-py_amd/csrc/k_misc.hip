@@ -128,6 +128,25 @@ __global__ __launch_bounds__(256) void k_stats(const flacmi_unit_meta* __restric
         if (h[i]) atomicAdd(&stats[i], h[i]);
 }
 
+/* ---- pipeline hand-off: a sub-batch's frame offsets and status into page-locked, mapped
+ * host memory (flacmi_encode_pipeline), written by the kernel over PCIe so the tiny copy
+ * never queues on a DMA engine behind the frame bytes ---- */
+__global__ __launch_bounds__(256) void k_export(const int64_t* __restrict__ off, const int32_t* __restrict__ st,
+                                                int64_t nf, int64_t* h_off, int32_t* h_st) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= nf; i += (int64_t)gridDim.x * blockDim.x) {
+        h_off[i] = off[i];
+        if (i < nf) h_st[i] = st[i];
+    }
+}
+
+hipError_t launch_export(const int64_t* off, const int32_t* st, int64_t nf, int64_t* h_off, int32_t* h_st,
+                         hipStream_t s) {
+    const int64_t blocks = (nf + 256) / 256;
+    hipLaunchKernelGGL(k_export, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s, off, st, nf, h_off,
+                       h_st);
+    return hipGetLastError();
+}
+
 /* ---- LDS poisoning (test knob FLACMI_POISON_LDS=<hex pattern>, read once per process) ----
  * Before every analysis kernel launch, one 160 KB workgroup per CU slot fills the LDS with a
  * pattern derived from <pattern>, so a kernel that reads LDS words it never wrote sees
