@@ -513,10 +513,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         if (prune) {
             /* tier 0: the wave's blocks k % 4 == 0 run the LPC groups (bound) beside the fixed
              * group; tiers 1..3 (only while the bound has not decided) add k % 4 == 2, 1, 3 */
+            const bool no_lpc = a.stop_after == 12; /* ablation (timing only): no LPC bound at all */
             for (int k = wid == 0 ? 1 : 0; k < kw; ++k) {
                 const h8 A = a_frag(ld(wid + k * nw));
                 blockA(I0{}, I0{}, I0{}, A, false);
-                if ((k & 3) == 0) blockA(I1{}, ING{}, I0{}, A, false);
+                if ((k & 3) == 0 && !no_lpc) blockA(I1{}, ING{}, I0{}, A, false);
             }
             if (wid == 0) block(I0{}, ING{}, I0{}, ld(0), true);
             reduce_store(I0{}, I1{});
@@ -542,7 +543,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                 for (int t = 1;; ++t) {
                     const uint64_t lb = tj > (uint64_t)n ? tj - (uint64_t)n : 0ull;
                     const uint64_t open = __ballot(lane >= 16 && lane < 16 + L && lb <= fmin);
-                    pruned = open == 0;
+                    pruned = open == 0 || a.stop_after >= 11; /* 11, 12: ablation, tier 0 only */
                     if (pruned || t == 4) break;
                     /* the next quarter of the blocks (k % 4 == 2, 1, 3; block 0 is in tier 0), only
                      * for the groups that hold an undecided order (mostly order 1's) */
@@ -678,8 +679,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             zp[j][0] = zp[j][1] = zp[j][2] = zp[j][3] = 0;
             if (c < nch) {
                 uint32_t z[8];
-                if constexpr (KK >= 0) fixed_chunk<KK>(xs, 8 * c, z);
-                else lpc_chunk(xs, 8 * c, coefl, lsh, order, z);
+                fixed_chunk<KK>(xs, 8 * c, z);
                 reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{z[0], z[1], z[2], z[3]};
                 reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{z[4], z[5], z[6], z[7]};
                 const uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
@@ -690,6 +690,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             }
         }
     };
+    /* the LPC predictor (rare: it wins only where the reference's sign convention lets it):
+     * one chunk per iteration, not unrolled, every chunk marked for the Rice pass's recompute
+     * path (code size: one inlined copy of the 12-tap predictor instead of kSCPT) */
+    auto residual_pass_lpc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < kSCPT; ++j) zp[j][0] = zp[j][1] = zp[j][2] = zp[j][3] = 0;
+#pragma unroll 1
+        for (int j = 0; j < kSCPT; ++j) {
+            const int c = tid + j * NT;
+            if (c < nch) {
+                uint32_t z[8];
+                lpc_chunk(xs, 8 * c, coefl, lsh, order, z);
+                reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{z[0], z[1], z[2], z[3]};
+                reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{z[4], z[5], z[6], z[7]};
+                const uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
+                if (omax >= 0) atomicAdd(&pks[(int)(((float)c + 0.5f) * inv_cpp)], cs);
+                big |= 1u << j;
+            }
+        }
+    };
     switch (fixed_k) {
         case 0: residual_pass(std::integral_constant<int, 0>{}); break;
         case 1: residual_pass(std::integral_constant<int, 1>{}); break;
@@ -697,7 +717,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         case 3: residual_pass(std::integral_constant<int, 3>{}); break;
         case 4: residual_pass(std::integral_constant<int, 4>{}); break;
         default:
-            if constexpr (NG > 0) residual_pass(std::integral_constant<int, -1>{});
+            if constexpr (NG > 0) residual_pass_lpc();
             break;
     }
     __syncthreads(); /* B3 */
@@ -782,17 +802,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                             tb[o2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, zp[jc][i]) >> sv, us2{1, 1}, tb[o2],
                                                             false);
                     }
-            } else {
-                uint32_t z[8];
-                resid(c, z);
-#pragma unroll
-                for (int o2 = 0; o2 < kRiceOrders; ++o2)
-                    if (o2 >= ro && o2 <= oo) {
-                        const uint32_t sh = pv[o2] & 0xffffu;
-                        tb[o2] += (z[0] >> sh) + (z[1] >> sh) + (z[2] >> sh) + (z[3] >> sh) + (z[4] >> sh) +
-                                  (z[5] >> sh) + (z[6] >> sh) + (z[7] >> sh);
-                    }
             }
+        }
+    }
+    /* rare: chunks holding a value >= 2^16 recompute their residual, in one loop that is not
+     * unrolled (one inlined copy of the six predictors instead of one per chunk slot: the
+     * kernel's code, and its instruction-cache footprint, shrink by a third) */
+    if (big) {
+#pragma unroll 1
+        for (int jc = 0; jc < kSCPT; ++jc) {
+            if (!((big >> jc) & 1)) continue;
+            const int c = tid + jc * NT;
+            const int k = (int)(((float)c + 0.5f) * inv_cpp);
+            const uint4 pq = *reinterpret_cast<const uint4*>(pkw + k * kRiceOrders);
+            const uint32_t pw[4] = {pq.x, pq.y, pq.z, pq.w};
+            uint32_t z[8];
+            resid(c, z);
+#pragma unroll
+            for (int o2 = 0; o2 < kRiceOrders; ++o2)
+                if (o2 >= ro && o2 <= oo) {
+                    const uint32_t sh = (pw[o2 >> 1] >> (16 * (o2 & 1))) & 0xffffu;
+                    tb[o2] += (z[0] >> sh) + (z[1] >> sh) + (z[2] >> sh) + (z[3] >> sh) + (z[4] >> sh) +
+                              (z[5] >> sh) + (z[6] >> sh) + (z[7] >> sh);
+                }
         }
     }
     {
