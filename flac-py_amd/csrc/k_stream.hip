@@ -69,23 +69,35 @@ struct SLds {
  * config-2 unit (n = 4608, two waves) at 10160 B: 16 workgroups per CU.
  *   xs   biased samples behind a 16-sample zero pad             staging .. Rice recompute
  *   pk   u16 [P][order] Rice parameters                         Rice (after B3)
- *   rec  the unit's LPC record (aliases pk)                     staging .. choice (before B3)
+ *   rec  the LPC orders' f16 tap table (aliases pk, tap_table)  staging .. MFMA operands
  *   red  u64 [nw][group][order] MFMA partial sums               MFMA phase .. choice
  *   red2 u64 [nw + 1][order] data bits (aliases red)            Rice (after B3)
  *   red0 u32 [nw] sum|x|                                         staging .. choice
  *   pks  u32 [P] finest partition sums                          staging (zeroed) .. Rice */
-__host__ __device__ inline SLds stream_lds(int n, int nw, int rec_words, int P) {
+__host__ __device__ inline SLds stream_lds(int n, int nw, int tap_words, int P) {
     auto up = [](int b) { return (b + 15) & ~15; };
     auto mx = [](int x, int y) { return x > y ? x : y; };
     SLds l;
     int o = 0;
     l.xs = o;   o = up(o + 2 * (kSHP + n));
-    l.pk = l.rec = o; o = up(o + mx(2 * P * kRiceOrders, 4 * mx(rec_words, 1)));
+    l.pk = l.rec = o; o = up(o + mx(2 * P * kRiceOrders, 4 * mx(tap_words, 1)));
     l.red = l.red2 = o; o = up(o + mx(8 * nw * 16, 8 * (nw + 1) * kRiceOrders));
     l.red0 = o; o = up(o + 4 * nw);
     l.pks = o;  o = up(o + 4 * P);
     l.total = o;
     return l;
+}
+
+/* The LPC orders' taps as an f16 table, built in staging straight from the global record
+ * (encoder.py:537-548 prediction_residual as taps: T_p[0] = -2^shift_p for x[i] itself,
+ * T_p[m] = c_p[m - 1] for x[i - m], 0 elsewhere).  Row p (1 .. 4 NG) holds the halves
+ * D_p[k] = T_p[16 - k], k = 0 .. 21, from word 10 (p - 1): descending tap order, so a lane's
+ * operand pairs (T[i], T[i-1]) are consecutive halves (one v_alignbit off a dword edge).  Rows
+ * overlap by one word (k = 20, 21 of row p = k = 0, 1 of row p + 1: zero in both for p <= 12),
+ * rows p > L are zero. */
+__host__ __device__ constexpr int tap_table_words(int NG) { return NG > 0 ? 40 * NG + 1 : 0; }
+__device__ __forceinline__ uint32_t f16_of_int(int v) {
+    return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)(float)v); /* exact for |v| <= 2048 */
 }
 
 /* f16 bit pattern of a small integer (exact) */
@@ -280,7 +292,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (n % (1 << o) == 0) rmax_eff = o;
     const int Pmax = 1 << rmax_eff; /* host-checked: 0 <= rmax_eff <= 5 */
-    const SLds lay = stream_lds(n, nw, rw, Pmax);
+    const SLds lay = stream_lds(n, nw, tap_table_words(NG), Pmax);
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem + lay.xs) + kSHP;
     int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.rec);
     uint32_t* red0 = reinterpret_cast<uint32_t*>(smem + lay.red0);
@@ -300,11 +312,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
 #pragma unroll
         for (int j = 0; j < kSCPT; ++j) q[j] = src[min(tid + j * NT, nch - 1)];
         fixb = reinterpret_cast<const uint4*>(kFixB.w)[lane];
-        int32_t rv[2] = {0, 0};
+        /* tap table words tid + j NT: word w of row p holds (T_p[16 - 2w], T_p[15 - 2w]); the
+         * record values it needs are loaded here, with the samples (clamped, unconditional) */
+        constexpr int kTW = tap_table_words(NG), kTJ = NG > 0 ? (kTW + 63) / 64 : 0;
+        int32_t tv[kTJ > 0 ? kTJ : 1][2];
         if constexpr (NG > 0) {
             const int32_t* r = a.rec + gid * a.rec_words;
 #pragma unroll
-            for (int j = 0; j < 2; ++j) rv[j] = r[min(tid + j * NT, rw - 1)];
+            for (int j = 0; j < kTJ; ++j) {
+                const int gw = tid + j * NT, p = gw / 10 + 1, w = gw - 10 * (p - 1);
+                const int pc = p < L ? p : L, base = 2 + L + (pc * (pc - 1)) / 2;
+                /* T_p[16 - 2w] (the shift for w = 8: T_p[0] = -2^shift) and T_p[15 - 2w] */
+                tv[j][0] = r[w == 8 ? 1 + pc : min(max(base + 15 - 2 * w, 0), rw - 1)];
+                tv[j][1] = r[min(max(base + 14 - 2 * w, 0), rw - 1)];
+            }
         }
         if (tid < kSHP) xs[tid - kSHP] = 0x8000u; /* biased zeros */
         if (tid < Pmax) pks[tid] = 0;
@@ -325,9 +346,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             }
         }
         if constexpr (NG > 0) {
+            uint32_t* tt = reinterpret_cast<uint32_t*>(recl);
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-                if (tid + j * NT < rw) recl[tid + j * NT] = rv[j];
+            for (int j = 0; j < kTJ; ++j) {
+                const int gw = tid + j * NT, p = gw / 10 + 1, w = gw - 10 * (p - 1);
+                if (gw < kTW) {
+                    auto tap = [&](int i, int32_t c) -> uint32_t {
+                        if (p > L || i < 0 || i > p) return 0u;
+                        return f16_of_int(i == 0 ? -(1 << c) : c);
+                    };
+                    tt[gw] = tap(16 - 2 * w, tv[j][0]) | tap(15 - 2 * w, tv[j][1]) << 16;
+                }
+            }
         }
         const uint32_t sx = wave_sum_u32(sumx);
         if (lane == 0) red0[wid] = sx;
@@ -338,8 +368,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     /* ---- unit status from the LPC record; MFMA exactness bound per order.
      * Every wave reads the same LDS words, so the exits are workgroup-uniform. ---- */
     uint32_t negmask = 0;
+    const int32_t* __restrict__ grec = NG > 0 ? a.rec + gid * a.rec_words : nullptr; /* wave-uniform: scalar loads */
     if constexpr (NG > 0) {
-        const int st = recl[0];
+        const int st = grec[0];
         if (st != 0) { /* the reference raises inside encode_subframe_lpc */
             if (wid == 0) {
                 mv.status = st & 0xffff;
@@ -348,28 +379,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             }
             return;
         }
-        negmask = (uint32_t)recl[1];
-        int sa = 0; /* lane p - 1: (sum|c| + 2^shift) of order p; * 33023 < 2^22 keeps the MFMA exact */
-        if (lane < L) {
-            const int p = lane + 1, sh = recl[2 + lane];
-            const int32_t* cp = recl + 2 + L + (p * (p - 1)) / 2;
-            int c[4 * NG];
-#pragma unroll
-            for (int m = 0; m < 4 * NG; ++m) c[m] = m < p ? cp[m] : 0; /* independent reads */
-            sa = 1 << sh;
-#pragma unroll
-            for (int m = 0; m < 4 * NG; ++m) sa += c[m] < 0 ? -c[m] : c[m];
-        }
-        if (__ballot(sa > kCoefLimit)) { /* outside the exactness bound: k_resid redoes it */
-            if (tid == 0) {
-                meta->status = FLACMI_STATUS_RETRY;
-                const unsigned long long k = atomicAdd(a.retry_count, 1ull);
-                a.retry_list[k] = gid;
-            }
-            return;
-        }
+        negmask = (uint32_t)grec[1];
     }
-    if (a.stop_after == 1) return;
 
     /* ---- candidate sums on MFMA ----
      * Exact mode: every block runs all NG + 1 groups and the LPC values are exact
@@ -409,41 +420,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     {
         const int col = lane & 15, kb = lane >> 4, o4 = col >> 2, rho = col & 3;
         h8 B[NG + 1];
-        int shg[NG + 1];
-        uint32_t kg[NG + 1];
-        const int idx0 = 12 + rho - 4 * kb + 2; /* tap index of the lane's first operand pair, + 2 */
+        int shg[NG + 1]; /* (kMagicBits >> shift is recomputed per block in exact mode: one VGPR per group fewer) */
+        /* LPC groups: the lane's taps T[ia] .. T[ia-3] (ia = 12 + rho - 4 kb) are the halves
+         * D[16 - ia] .. D[19 - ia] of its order's tap-table row: three dwords and two
+         * v_alignbit.  The exactness bound (sum|c| + 2^shift) * 33023 < 2^22 is read off the
+         * same registers: the lanes with rho = 0 hold disjoint windows [ia - 3, ia] covering
+         * taps -3 .. 12, so their |halves| summed over kb give sum_m |T_p[m]|. */
+        const uint32_t* tt = reinterpret_cast<const uint32_t*>(recl);
+        const int k0 = 4 + 4 * kb - rho; /* 16 - ia */
+        const uint32_t alb = 16u * (uint32_t)(k0 & 1);
+        bool outside = false;
 #pragma unroll
         for (int g = 0; g <= NG; ++g) {
+            int sh = 0;
             if (g == 0) {
                 B[0] = __builtin_bit_cast(h8, fixb);
-            } else { /* taps T[ia], T[ia-1], T[ia-2], T[ia-3] of LPC order p from the record */
-                const int p = 4 * (g - 1) + o4 + 1, ia = idx0 - 2;
-                const bool live = p <= L;
-                const int sh = live ? recl[2 + p - 1] : 0;
-                const int32_t* cp = recl + 2 + L + (p * (p - 1)) / 2;
-                float t[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int m = ia - u;
-                    int v = 0;
-                    if (m == 0) v = -(1 << sh);
-                    else if (m >= 1 && m <= p) v = cp[m - 1];
-                    t[u] = live ? (float)v : 0.0f;
-                }
-                const uint32_t l0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t[0], t[1]));
-                const uint32_t l2 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(t[2], t[3]));
-                const uint32_t h0 = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[0], 256.0f * t[1]));
-                const uint32_t hh = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(256.0f * t[2], 256.0f * t[3]));
+            } else {
+                const int p = 4 * (g - 1) + o4 + 1, wb = 10 * (p - 1) + (k0 >> 1);
+                const uint32_t w0 = tt[wb], w1 = tt[wb + 1], w2 = tt[wb + 2];
+                const uint32_t l0 = __builtin_amdgcn_alignbit(w1, w0, alb), l2 = __builtin_amdgcn_alignbit(w2, w1, alb);
+                const h2 k256{(_Float16)256.0f, (_Float16)256.0f};
+                const uint32_t h0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, l0) * k256);
+                const uint32_t hh = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, l2) * k256);
                 B[g] = __builtin_bit_cast(h8, uint4{h0, hh, l0, l2});
-            }
-            int sh = 0;
-            if (g > 0) {
-                const int p = 4 * (g - 1) + o4 + 1;
-                sh = p <= L ? recl[2 + p - 1] : 0;
+                /* sum|T| of this window, then over the four kb rows (lanes 16 apart) */
+                const h2 one{(_Float16)1.0f, (_Float16)1.0f};
+                float sw = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, l0 & 0x7fff7fffu), one, 0.0f, false);
+                sw = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, l2 & 0x7fff7fffu), one, sw, false);
+                sw += __shfl_xor(sw, 16);
+                sw += __shfl_xor(sw, 32);
+                outside |= rho == 0 && p <= L && sw > (float)kCoefLimit;
+                /* the shift from T_p[0] = -2^shift (half D[16], word 10 (p - 1) + 8) */
+                const uint32_t t0 = tt[10 * (p - 1) + 8] & 0xffffu;
+                sh = p <= L ? (int)((t0 >> 10) & 31u) - 15 : 0;
             }
             shg[g] = sh;
-            kg[g] = kMagicBits >> sh;
         }
+        if (NG > 0 && __ballot(outside)) { /* outside the MFMA exactness bound: k_resid redoes it */
+            if (tid == 0) {
+                meta->status = FLACMI_STATUS_RETRY;
+                const unsigned long long k = atomicAdd(a.retry_count, 1ull);
+                a.retry_list[k] = gid;
+            }
+            return;
+        }
+        if (a.stop_after == 1) return;
         /* first residual index of group g's order at this lane (block 0 only) */
         auto start_of = [&](int g) __attribute__((always_inline)) -> int {
             const int p = 4 * (g > 0 ? g - 1 : 0) + o4 + 1;
@@ -458,6 +479,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         auto ld = [&](int blk) __attribute__((always_inline)) {
             return *reinterpret_cast<const uint2*>(xs + 64 * blk + eoff);
         };
+        /* block 0 (masked, once per unit after the loop): its address recomputed from the
+         * thread id, so no VGPR holds it across the loop (at 64 VGPRs one would spill) */
+        auto ld0 = [&]() __attribute__((always_inline)) {
+            const uint32_t t = opaque((uint32_t)tid);
+            return *reinterpret_cast<const uint2*>(xs + 4 * (int)(t & 15) - 12 + 4 * (int)((t >> 4) & 3));
+        };
         /* one 64-sample block through the MFMAs of groups G0..G1; EX: LPC values exact, else
          * the bound |T| */
         auto blockA = [&](auto g0c, auto g1c, auto exc, const h8 A, bool masked) __attribute__((always_inline)) {
@@ -467,7 +494,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
 #pragma unroll
             for (int g = G0; g <= G1; ++g) D[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[g], C, 0, 0, 0);
 #pragma unroll
-            for (int g = G0; g <= G1; ++g)
+            for (int g = G0; g <= G1; ++g) {
+                const uint32_t kgv = kMagicBits >> shg[g];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     /* (a bit_cast of a vector element reads element 0: clang bug) */
@@ -475,14 +503,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                     if (masked) {
                         const int i = 4 * (4 * kb + r) + rho; /* block 0 */
                         const uint32_t sv =
-                            (g == 0 || !EX) ? sad32(bits, mbv, 0u) : sad32(bits >> shg[g], kg[g], 0u);
+                            (g == 0 || !EX) ? sad32(bits, mbv, 0u) : sad32(bits >> shg[g], kgv, 0u);
                         acc[g] += i >= start_of(g) ? sv : 0u;
                     } else if (g == 0 || !EX) { /* opaque: one v_sad_u32 per value, not a reassociated min/max/sub */
                         acc[g] = opaque(sad32(bits, mbv, acc[g]));
                     } else {
-                        acc[g] = sad32(bits >> shg[g], kg[g], acc[g]);
+                        acc[g] = sad32(bits >> shg[g], kgv, acc[g]);
                     }
                 }
+            }
         };
         auto block = [&](auto g0c, auto g1c, auto exc, uint2 q, bool masked) __attribute__((always_inline)) {
             blockA(g0c, g1c, exc, a_frag(q), masked);
@@ -519,11 +548,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                 blockA(I0{}, I0{}, I0{}, A, false);
                 if ((k & 3) == 0 && !no_lpc) blockA(I1{}, ING{}, I0{}, A, false);
             }
-            if (wid == 0) block(I0{}, ING{}, I0{}, ld(0), true);
+            if (wid == 0) block(I0{}, ING{}, I0{}, ld0(), true);
             reduce_store(I0{}, I1{});
         } else {
             for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I0{}, ING{}, I1{}, ld(blk), false);
-            if (wid == 0) block(I0{}, ING{}, I1{}, ld(0), true);
+            if (wid == 0) block(I0{}, ING{}, I1{}, ld0(), true);
             reduce_store(I0{}, I0{});
         }
         __syncthreads(); /* B2 */
@@ -569,7 +598,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
 #pragma unroll
                     for (int g = 1; g <= NG; ++g) acc[g] = 0;
                     for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I1{}, ING{}, I1{}, ld(blk), false);
-                    if (wid == 0) block(I1{}, ING{}, I1{}, ld(0), true);
+                    if (wid == 0) block(I1{}, ING{}, I1{}, ld0(), true);
                     reduce_store(I1{}, I0{});
                     __syncthreads();
                     tj = lane_total();
@@ -635,9 +664,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     mv.order = lpc_wins ? lbest : fo;
     if constexpr (NG > 0) {
         if (lpc_wins) {
-            mv.shift = recl[2 + lbest - 1];
+            mv.shift = grec[2 + lbest - 1];
             mv.ncoefs = lbest;
-            if (lane < lbest) coefl = recl[2 + L + (lbest * (lbest - 1)) / 2 + lane];
+            if (lane < lbest) coefl = grec[2 + L + (lbest * (lbest - 1)) / 2 + lane];
         }
     }
     if (a.stop_after == 3) return;
@@ -900,8 +929,6 @@ bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes) {
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
     if (rmax_eff < 0 || (1 << rmax_eff) > 32 || ((a.n >> rmax_eff) & 7) != 0) return false; /* heap nodes < 64 */
-    const int nt = stream_threads(a.n);
-    if (ref && a.rec_words > 2 * nt) return false;
     return true;
 }
 
@@ -911,7 +938,7 @@ static hipError_t launch_stream_R(const ResidArgs& a, hipStream_t s) {
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
-    const size_t lds = stream_lds(a.n, nt / 64, NG > 0 ? a.rec_words : 0, 1 << rmax_eff).total;
+    const size_t lds = stream_lds(a.n, nt / 64, tap_table_words(NG), 1 << rmax_eff).total;
     auto kern = k_resid_stream<NG, R05>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
