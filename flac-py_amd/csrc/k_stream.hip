@@ -159,14 +159,20 @@ __device__ __forceinline__ uint32_t h2sub(uint32_t t, float c) {
     return __builtin_bit_cast(uint32_t, v);
 }
 
-/* A fragment of one lane from 4 biased samples (two dwords): f16 high bytes (signed, via
- * (1024 + hb) - 1152) then f16 low bytes ((1024 + l) - 1024), all exact. */
-__device__ __forceinline__ h8 a_frag(uint2 q) {
-    const uint32_t hx = __builtin_amdgcn_perm(0x64646464u, q.x, 0x04030401u);
-    const uint32_t hy = __builtin_amdgcn_perm(0x64646464u, q.y, 0x04030401u);
-    const uint32_t lx = __builtin_amdgcn_perm(0x64646464u, q.x, 0x04020400u);
-    const uint32_t ly = __builtin_amdgcn_perm(0x64646464u, q.y, 0x04020400u);
-    const uint4 v{h2sub(hx, 1152.0f), h2sub(hy, 1152.0f), h2sub(lx, 1024.0f), h2sub(ly, 1024.0f)};
+/* Raw A fragment of one lane from 4 biased samples (two dwords): the f16 values 1024 + hb
+ * (biased high bytes) then 1024 + l (low bytes), one v_perm per pair.  Raw, it stands for
+ * x + 295936 (256 * 1152 + 1024) per sample: the fixed group takes it as it is, because a
+ * fixed predictor's taps sum to zero ((1 - z^-1)^o), so the offset cancels, and its partial
+ * sums stay exact (|M +- 1279 * 257 * 8| < 2^24 for order 4, whose positive and negative
+ * taps each sum to 8). */
+__device__ __forceinline__ uint4 a_raw(uint2 q) {
+    return uint4{__builtin_amdgcn_perm(0x64646464u, q.x, 0x04030401u), __builtin_amdgcn_perm(0x64646464u, q.y, 0x04030401u),
+                 __builtin_amdgcn_perm(0x64646464u, q.x, 0x04020400u), __builtin_amdgcn_perm(0x64646464u, q.y, 0x04020400u)};
+}
+/* the exact A fragment (the LPC groups' taps do not sum to zero): signed high bytes
+ * (1024 + hb) - 1152, low bytes (1024 + l) - 1024, all exact */
+__device__ __forceinline__ h8 a_sub(uint4 r) {
+    const uint4 v{h2sub(r.x, 1152.0f), h2sub(r.y, 1152.0f), h2sub(r.z, 1024.0f), h2sub(r.w, 1024.0f)};
     return __builtin_bit_cast(h8, v);
 }
 
@@ -487,12 +493,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         };
         /* one 64-sample block through the MFMAs of groups G0..G1; EX: LPC values exact, else
          * the bound |T| */
-        auto blockA = [&](auto g0c, auto g1c, auto exc, const h8 A, bool masked) __attribute__((always_inline)) {
+        auto blockA = [&](auto g0c, auto g1c, auto exc, const uint4 Ar, bool masked) __attribute__((always_inline)) {
             constexpr int G0 = decltype(g0c)::value, G1 = decltype(g1c)::value;
             constexpr bool EX = decltype(exc)::value != 0;
             f4 D[NG + 1];
+            h8 A{};
+            if constexpr (G1 >= 1) A = a_sub(Ar);
 #pragma unroll
-            for (int g = G0; g <= G1; ++g) D[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[g], C, 0, 0, 0);
+            for (int g = G0; g <= G1; ++g)
+                D[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(g == 0 ? __builtin_bit_cast(h8, Ar) : A, B[g], C, 0, 0, 0);
 #pragma unroll
             for (int g = G0; g <= G1; ++g) {
                 const uint32_t kgv = kMagicBits >> shg[g];
@@ -514,7 +523,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             }
         };
         auto block = [&](auto g0c, auto g1c, auto exc, uint2 q, bool masked) __attribute__((always_inline)) {
-            blockA(g0c, g1c, exc, a_frag(q), masked);
+            blockA(g0c, g1c, exc, a_raw(q), masked);
         };
         /* per (group, order): sum over the 4 phases (quad, < 2^32) then, in 64 bits, over the
          * 4 kb rows; the lanes with rho == 0 and kb == 0 store.  BD: the LPC groups hold the
@@ -544,7 +553,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
              * group; tiers 1..3 (only while the bound has not decided) add k % 4 == 2, 1, 3 */
             const bool no_lpc = a.stop_after == 12; /* ablation (timing only): no LPC bound at all */
             for (int k = wid == 0 ? 1 : 0; k < kw; ++k) {
-                const h8 A = a_frag(ld(wid + k * nw));
+                const uint4 A = a_raw(ld(wid + k * nw));
                 blockA(I0{}, I0{}, I0{}, A, false);
                 if ((k & 3) == 0 && !no_lpc) blockA(I1{}, ING{}, I0{}, A, false);
             }
@@ -579,7 +588,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                     const uint32_t gneed = (uint32_t)(open >> 16);
                     __syncthreads(); /* every wave has read the bounds */
                     for (int k = t == 1 ? 2 : t == 2 ? 1 : 3; k < kw; k += 4) {
-                        const h8 A = a_frag(ld(wid + k * nw));
+                        const h8 A = a_sub(a_raw(ld(wid + k * nw)));
 #pragma unroll
                         for (int g = 1; g <= NG; ++g) {
                             if ((gneed >> (4 * (g - 1))) & 15u) {
@@ -860,13 +869,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         uint32_t any = 0;
 #pragma unroll
         for (int o2 = 0; o2 < kRiceOrders; ++o2) any |= (o2 >= ro && o2 <= oo) ? tb[o2] : 0u;
-        const bool narrow = __ballot(any >= (1u << 26)) == 0;
+        /* a wave-uniform branch, not a select: the 64-bit reduction (never taken by 16-bit
+         * data) would otherwise run beside the 32-bit one for every order */
+        if (__ballot(any >= (1u << 26)) == 0) {
 #pragma unroll
-        for (int o2 = 0; o2 < kRiceOrders; ++o2)
-            if (o2 >= ro && o2 <= oo) {
-                const uint64_t w = narrow ? (uint64_t)wave_sum_u32(tb[o2]) : wave_sum_u64(tb[o2]);
+            for (int o2 = 0; o2 < kRiceOrders; ++o2)
+                if (o2 >= ro && o2 <= oo) {
+                    const uint32_t w = wave_sum_u32(tb[o2]);
+                    if (lane == 0) red2[wid * kRiceOrders + o2] = w;
+                }
+        } else {
+#pragma unroll 1
+            for (int o2 = ro; o2 <= oo; ++o2) {
+                uint32_t t = 0;
+#pragma unroll
+                for (int o3 = 0; o3 < kRiceOrders; ++o3) t = o3 == o2 ? tb[o3] : t;
+                const uint64_t w = wave_sum_u64(t);
                 if (lane == 0) red2[wid * kRiceOrders + o2] = w;
             }
+        }
     }
     __syncthreads(); /* B4 */
     STAMP(6);
