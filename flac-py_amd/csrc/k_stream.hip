@@ -68,19 +68,19 @@ struct SLds {
 /* Workgroup LDS (bytes).  Regions whose lifetimes do not overlap share space, which keeps a
  * config-2 unit (n = 4608, two waves) at 10160 B: 16 workgroups per CU.
  *   xs   biased samples behind a 16-sample zero pad             staging .. Rice recompute
- *   pk   u16 [P][order] Rice parameters                         Rice (after B3)
+ *   pk   u32 [P][RS] Rice parameters p | p << 16 per order       Rice (after B3)
  *   rec  the LPC orders' f16 tap table (aliases pk, tap_table)  staging .. MFMA operands
  *   red  u64 [nw][group][order] MFMA partial sums               MFMA phase .. choice
  *   red2 u64 [nw + 1][order] data bits (aliases red)            Rice (after B3)
  *   red0 u32 [nw] sum|x|                                         staging .. choice
  *   pks  u32 [P] finest partition sums                          staging (zeroed) .. Rice */
-__host__ __device__ inline SLds stream_lds(int n, int nw, int tap_words, int P) {
+__host__ __device__ inline SLds stream_lds(int n, int nw, int tap_words, int P, int RS) {
     auto up = [](int b) { return (b + 15) & ~15; };
     auto mx = [](int x, int y) { return x > y ? x : y; };
     SLds l;
     int o = 0;
     l.xs = o;   o = up(o + 2 * (kSHP + n));
-    l.pk = l.rec = o; o = up(o + mx(2 * P * kRiceOrders, 4 * mx(tap_words, 1)));
+    l.pk = l.rec = o; o = up(o + mx(4 * P * RS, 4 * mx(tap_words, 1)));
     l.red = l.red2 = o; o = up(o + mx(8 * nw * 16, 8 * (nw + 1) * kRiceOrders));
     l.red0 = o; o = up(o + 4 * nw);
     l.pks = o;  o = up(o + 4 * P);
@@ -186,9 +186,17 @@ __device__ __forceinline__ int rice_param_exact(uint64_t s, int len) {
     return p;
 }
 
+/* one finest partition's Rice table row (32 bytes: p | p << 16 per order) */
+__device__ __forceinline__ void load_ptab(const uint32_t* row, uint32_t (&pv)[kRiceOrders]) {
+    const uint4 a = *reinterpret_cast<const uint4*>(row);
+    const uint4 b = *reinterpret_cast<const uint4*>(row + 4);
+    pv[0] = a.x, pv[1] = a.y, pv[2] = a.z, pv[3] = a.w;
+    pv[4] = b.x, pv[5] = b.y, pv[6] = b.z, pv[7] = b.w;
+}
+
 /* fixed order K residual of samples i0..i0+7 from biased LDS samples, zig-zagged; the
  * warm-up samples (i < K) give 0 */
-template <int K>
+template <int K, bool FIRST = true>
 __device__ __forceinline__ void fixed_chunk(const uint16_t* xs, int i0, uint32_t (&z)[8]) {
     const uint4 w = *reinterpret_cast<const uint4*>(xs + i0);
     const uint4 v = *reinterpret_cast<const uint4*>(xs + i0 - 8); /* pad >= 8 */
@@ -212,7 +220,7 @@ __device__ __forceinline__ void fixed_chunk(const uint16_t* xs, int i0, uint32_t
         const int32_t r = d[4 + k];
         z[k] = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
     }
-    if (i0 == 0) {
+    if (FIRST && i0 == 0) { /* only the first chunk slot can hold chunk 0 */
 #pragma unroll
         for (int k = 0; k < K; ++k) z[k] = 0;
     }
@@ -298,13 +306,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (n % (1 << o) == 0) rmax_eff = o;
     const int Pmax = 1 << rmax_eff; /* host-checked: 0 <= rmax_eff <= 5 */
-    const SLds lay = stream_lds(n, nw, tap_table_words(NG), Pmax);
+    constexpr int RS = kRiceOrders; /* Rice table words per finest partition (32-byte rows) */
+    const SLds lay = stream_lds(n, nw, tap_table_words(NG), Pmax, RS);
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem + lay.xs) + kSHP;
     int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.rec);
     uint32_t* red0 = reinterpret_cast<uint32_t*>(smem + lay.red0);
     unsigned long long* red2 = reinterpret_cast<unsigned long long*>(smem + lay.red2);
     uint32_t* pks = reinterpret_cast<uint32_t*>(smem + lay.pks); /* finest partition sums */
-    uint16_t* pkw = reinterpret_cast<uint16_t*>(smem + lay.pk);
+    uint32_t* pkw = reinterpret_cast<uint32_t*>(smem + lay.pk);
     flacmi_unit_meta* meta = a.meta + gid;
     MetaVals mv{};
 
@@ -690,7 +699,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         for (int o = a.rmin; o <= a.rmax; ++o)
             if ((n % (1 << o)) == 0 && (n >> o) > order) omax = o;
     const int P = 1 << (omax < 0 ? 0 : omax), cpp = (n >> (omax < 0 ? 0 : omax)) >> 3;
-    const float inv_cpp = 1.0f / (float)cpp;
+    /* finest partition of chunk c = floor(c / cpp) = mulhi(c, ceil(2^32 / cpp)): exact for c * cpp < 2^32 */
+    const uint32_t mcpp = (uint32_t)((0x100000000ull + (uint64_t)cpp - 1) / (uint64_t)cpp);
+    auto part_of = [&](int c) __attribute__((always_inline)) -> int { return (int)__umulhi((uint32_t)c, mcpp); };
     uint32_t* __restrict__ rout = reinterpret_cast<uint32_t*>(a.residual) + gid * a.residual_stride;
     const int fixed_k = __builtin_amdgcn_readfirstlane(lpc_wins ? -1 : order);
     const int lsh = mv.shift;
@@ -717,11 +728,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             zp[j][0] = zp[j][1] = zp[j][2] = zp[j][3] = 0;
             if (c < nch) {
                 uint32_t z[8];
-                fixed_chunk<KK>(xs, 8 * c, z);
+                if (j == 0) fixed_chunk<KK, true>(xs, 8 * c, z);
+                else fixed_chunk<KK, false>(xs, 8 * c, z);
                 reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{z[0], z[1], z[2], z[3]};
                 reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{z[4], z[5], z[6], z[7]};
                 const uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
-                if (omax >= 0) atomicAdd(&pks[(int)(((float)c + 0.5f) * inv_cpp)], cs);
+                if (omax >= 0) atomicAdd(&pks[part_of(c)], cs);
                 if ((z[0] | z[1] | z[2] | z[3] | z[4] | z[5] | z[6] | z[7]) >> 16) big |= 1u << j;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) zp[j][i] = __builtin_amdgcn_perm(z[2 * i + 1], z[2 * i], 0x05040100u);
@@ -743,7 +755,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                 reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{z[0], z[1], z[2], z[3]};
                 reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{z[4], z[5], z[6], z[7]};
                 const uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
-                if (omax >= 0) atomicAdd(&pks[(int)(((float)c + 0.5f) * inv_cpp)], cs);
+                if (omax >= 0) atomicAdd(&pks[part_of(c)], cs);
                 big |= 1u << j;
             }
         }
@@ -775,10 +787,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     /* every wave, lane j - 1 = heap node j = (order o, partition K), j = 2^o + K < 2P <= 64:
      * node sums from a prefix over the finest sums, one parameter each, the first error in
      * the reference's evaluation order = the lowest node (orders ascending, then partitions) */
-    uint64_t pre = lane < P ? (uint64_t)pks[lane] : 0;
+    /* 32 bits: the chosen predictor's sum|r| is at most the order-0 sum n * 2^15, so its
+     * zig-zag total stays below 2 * 10240 * 2^15 + n < 2^32 */
+    uint32_t pre = lane < P ? pks[lane] : 0u;
 #pragma unroll
     for (int d = 1; d < 32; d <<= 1) {
-        const uint64_t t = (uint64_t)__shfl_up((unsigned long long)pre, (unsigned)d);
+        const uint32_t t = (uint32_t)__shfl_up((int)pre, (unsigned)d);
         if (lane >= d) pre += t;
     }
     const int j = lane + 1;
@@ -786,12 +800,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     const int K = j - (1 << o), dd = oo - o;
     const bool valid = j < 2 * P && o >= ro;
     const int hi_k = ((K + 1) << (dd < 0 ? 0 : dd)) - 1, lo_k = (K << (dd < 0 ? 0 : dd)) - 1;
-    const uint64_t ph = (uint64_t)__shfl((unsigned long long)pre, hi_k & 63);
-    const uint64_t pl = (uint64_t)__shfl((unsigned long long)pre, lo_k & 63);
-    const uint64_t snode = ph - (lo_k >= 0 ? pl : 0ull);
+    const uint32_t ph = (uint32_t)__shfl((int)pre, hi_k & 63);
+    const uint32_t pl = (uint32_t)__shfl((int)pre, lo_k & 63);
+    const uint32_t snode = ph - (lo_k >= 0 ? pl : 0u);
     const int len = (n >> (o < 16 ? o : 15)) - (K == 0 ? order : 0);
     const bool zero = snode == 0;
-    const int prm = (zero || !valid) ? 0 : rice_param_exact(snode, len);
+    const int prm = (zero || !valid) ? 0 : rice_param_exact((uint64_t)snode, len);
     {
         const unsigned long long eb = __ballot(valid && (zero || prm < 0));
         if (eb) {
@@ -811,7 +825,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         if (o2 >= ro && o2 <= oo) {
             const int node = (1 << o2) + (lane >> (oo - o2));
             const int pv = __shfl(prm, (node - 1) & 63);
-            if (lane < P) pkw[lane * kRiceOrders + o2] = (uint16_t)pv;
+            if (lane < P) pkw[lane * RS + o2] = (uint32_t)pv * 0x10001u;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -823,13 +837,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     for (int jc = 0; jc < kSCPT; ++jc) {
         const int c = tid + jc * NT;
         if (c < nch) {
-            const int k = (int)(((float)c + 0.5f) * inv_cpp);
-            const uint4 pq = *reinterpret_cast<const uint4*>(pkw + k * kRiceOrders);
-            const uint32_t pw[4] = {pq.x, pq.y, pq.z, pq.w};
-            uint32_t pv[8]; /* p | p << 16 per order */
-#pragma unroll
-            for (int o2 = 0; o2 < kRiceOrders; ++o2)
-                pv[o2] = __builtin_amdgcn_perm(pw[o2 >> 1], pw[o2 >> 1], (o2 & 1) ? 0x03020302u : 0x01000100u);
+            const int k = part_of(c);
+            uint32_t pv[kRiceOrders]; /* p | p << 16 per order */
+            load_ptab(pkw + k * RS, pv);
             if (!((big >> jc) & 1)) {
 #pragma unroll
                 for (int o2 = 0; o2 < kRiceOrders; ++o2)
@@ -851,15 +861,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         for (int jc = 0; jc < kSCPT; ++jc) {
             if (!((big >> jc) & 1)) continue;
             const int c = tid + jc * NT;
-            const int k = (int)(((float)c + 0.5f) * inv_cpp);
-            const uint4 pq = *reinterpret_cast<const uint4*>(pkw + k * kRiceOrders);
-            const uint32_t pw[4] = {pq.x, pq.y, pq.z, pq.w};
+            const int k = part_of(c);
+            uint32_t pw[kRiceOrders];
+            load_ptab(pkw + k * RS, pw);
             uint32_t z[8];
             resid(c, z);
 #pragma unroll
             for (int o2 = 0; o2 < kRiceOrders; ++o2)
                 if (o2 >= ro && o2 <= oo) {
-                    const uint32_t sh = (pw[o2 >> 1] >> (16 * (o2 & 1))) & 0xffffu;
+                    const uint32_t sh = pw[o2] & 0xffffu;
                     tb[o2] += (z[0] >> sh) + (z[1] >> sh) + (z[2] >> sh) + (z[3] >> sh) + (z[4] >> sh) +
                               (z[5] >> sh) + (z[6] >> sh) + (z[7] >> sh);
                 }
@@ -872,11 +882,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         /* a wave-uniform branch, not a select: the 64-bit reduction (never taken by 16-bit
          * data) would otherwise run beside the 32-bit one for every order */
         if (__ballot(any >= (1u << 26)) == 0) {
+            /* DPP row reductions; lane 63 holds the wave total and stores it (no readlane) */
 #pragma unroll
             for (int o2 = 0; o2 < kRiceOrders; ++o2)
                 if (o2 >= ro && o2 <= oo) {
-                    const uint32_t w = wave_sum_u32(tb[o2]);
-                    if (lane == 0) red2[wid * kRiceOrders + o2] = w;
+                    uint32_t v = tb[o2];
+                    v += dpp_u32<0xB1, 0xf>(v);
+                    v += dpp_u32<0x4E, 0xf>(v);
+                    v += dpp_u32<0x141, 0xf>(v);
+                    v += dpp_u32<0x140, 0xf>(v);
+                    v += dpp_u32<0x142, 0xa>(v);
+                    v += dpp_u32<0x143, 0xc>(v);
+                    if (lane == 63) red2[wid * kRiceOrders + o2] = v;
                 }
         } else {
 #pragma unroll 1
@@ -891,6 +908,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     }
     __syncthreads(); /* B4 */
     STAMP(6);
+#if defined(FLACMI_PAD_VALU) /* diagnostic build only: extra independent VALU per unit (price of issue) */
+    {
+        uint32_t q0 = lane, q1 = lane ^ 5u, q2 = lane * 3u, q3 = lane + 7u;
+#pragma unroll
+        for (int i = 0; i < FLACMI_PAD_VALU / 8; ++i)
+            asm volatile("v_add_u32 %0, %0, %4\n v_add_u32 %1, %1, %4\n v_add_u32 %2, %2, %4\n v_add_u32 %3, %3, %4"
+                         : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3) : "v"(lane));
+        if ((q0 ^ q1 ^ q2 ^ q3) == 0xdeadbeefu) meta->reserved0 = 1;
+    }
+#endif
+#if defined(FLACMI_PAD_SALU) /* diagnostic build only: extra SALU per unit */
+    {
+        uint32_t q0 = (uint32_t)gid, q1 = (uint32_t)gid ^ 5u;
+#pragma unroll
+        for (int i = 0; i < FLACMI_PAD_SALU / 4; ++i)
+            asm volatile("s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5" : "+s"(q0), "+s"(q1));
+        if ((q0 ^ q1) == 0xdeadbeefu) meta->reserved0 = 1;
+    }
+#endif
     if (wid != 0) return;
     /* wave 0: headers per order (lanes of that order's nodes), totals, first minimum */
     const uint32_t hb = valid ? 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm) : 0u;
@@ -932,7 +968,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     }
 #endif
     int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
-    if (lane < (1 << best)) rp[lane] = (int32_t)pkw[(lane << (oo - best)) * kRiceOrders + best];
+    if (lane < (1 << best)) rp[lane] = (int32_t)(pkw[(lane << (oo - best)) * RS + best] & 0xffffu);
 }
 
 /* units the stream kernel listed (outside its MFMA bound) are handled by k_resid's list
@@ -959,7 +995,7 @@ static hipError_t launch_stream_R(const ResidArgs& a, hipStream_t s) {
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
-    const size_t lds = stream_lds(a.n, nt / 64, tap_table_words(NG), 1 << rmax_eff).total;
+    const size_t lds = stream_lds(a.n, nt / 64, tap_table_words(NG), 1 << rmax_eff, kRiceOrders).total;
     auto kern = k_resid_stream<NG, R05>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
