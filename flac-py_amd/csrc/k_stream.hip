@@ -153,6 +153,11 @@ __device__ __forceinline__ uint32_t opaque(uint32_t v) {
     asm volatile("" : "+v"(v));
     return v;
 }
+/* a wave-uniform constant kept opaque in an SGPR (v_sad_u32 takes it as src1) */
+__device__ __forceinline__ uint32_t opaque_s(uint32_t v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
 
 __device__ __forceinline__ uint32_t h2sub(uint32_t t, float c) {
     const h2 v = __builtin_bit_cast(h2, t) - h2{(_Float16)c, (_Float16)c};
@@ -485,7 +490,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             const int p = 4 * (g > 0 ? g - 1 : 0) + o4 + 1;
             return (g > 0 && ((negmask >> (p - 1)) & 1)) ? 0 : p;
         };
-        const uint32_t mbv = opaque(kMagicBits);
+        const uint32_t mbv = opaque_s(kMagicBits);
         const f4 C{12582912.0f, 12582912.0f, 12582912.0f, 12582912.0f};
         const int eoff = 4 * (lane & 15) - 12 + 4 * kb;
         uint32_t acc[NG + 1];
