@@ -22,6 +22,7 @@ namespace flacmi {
 enum { PATH_S16 = 0, PATH_N32 = 1, PATH_W64 = 2, PATH_W64S = 3 };
 
 typedef short short2v __attribute__((ext_vector_type(2)));
+typedef unsigned short us2x __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int32_t sdot2(uint32_t a, uint32_t b, int32_t c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, a), __builtin_bit_cast(short2v, b), c, false);
@@ -566,8 +567,8 @@ __device__ __forceinline__ void mf8_tile_epilogue(const v4i (&D)[4], int s, cons
  * 8-sample chunks, into red[wid][0..4]).  pl: the three digit planes, PLB bytes apart;
  * cfl / lsh: phase A's coefficient and shift tables; G: tiles per u32 partial sum.
  *
- * prune (reference mode): the tiles run in four tiers, the wave's tiles k % 4 == 0, then
- * 2, 1, 3.  After each tier every wave reads the workgroup's exact partial LPC sums (a sum
+ * prune (reference mode): the tiles run in eight tiers, the wave's tiles k % 8 == 0, then
+ * 4, 2, 6, 1, 5, 3, 7.  After each tier every wave reads the workgroup's exact partial LPC sums (a sum
  * over a subset of the values, so a lower bound of each order's full sum) against the best
  * exact fixed sum; once every order's partial sum exceeds it, LPC can neither win nor tie
  * (encoder.py:135-157) and the remaining tiers are skipped: returns true (workgroup-uniform;
@@ -758,11 +759,17 @@ __device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const un
         return false;
     }
     bool pruned = false;
+    /* eighths of the wave's tiles, spread over the block (residues 0, 4, 2, 6, 1, 5, 3, 7 of
+     * the wave's tile index mod 8): a unit stops at the first eighth whose partial LPC sums
+     * all exceed the best fixed sum (config 3: LPC sums run ~4x the fixed ones, so most
+     * units stop after two or three eighths) */
+    constexpr int kTiers = 8;
 #pragma unroll 1
-    for (int t = 0; t < 4; ++t) {
-        go(wid + (t == 0 ? 0 : t == 1 ? 2 : t == 2 ? 1 : 3) * nw, 4 * nw);
+    for (int t = 0; t < kTiers; ++t) {
+        const int res = (int)((0x73516240u >> (4 * t)) & 15u);
+        go(wid + res * nw, kTiers * nw);
         store();
-        if (t == 3) break; /* every tile done: the sums are exact */
+        if (t == kTiers - 1) break; /* every tile done: the sums are exact */
         __syncthreads();
         uint64_t tj = 0;
         if (lane < NSUM)
@@ -1872,19 +1879,66 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             }
             const int cpp = ps >> 3;
             const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+            /* each finest partition's row: byte o = p_o - pm for the candidate orders, byte 15 =
+             * pm = their smallest parameter (orders <= 12, so byte 15 is free).  Then
+             * sum(z >> p_o) = sum(y >> (p_o - pm)) with y = z >> pm, and y mostly fits 16 bits:
+             * two values per v_pk_lshrrev_b16 + v_dot2_u32_u16 */
+            for (int k = tid; k < P; k += NT) {
+                uint32_t* r = reinterpret_cast<uint32_t*>(pk + 16 * k);
+                uint32_t w[4] = {r[0], r[1], r[2], r[3]};
+                uint32_t pm = 255;
+#pragma unroll
+                for (int o = 0; o < 13; ++o)
+                    if (o >= ro && o <= oo) pm = min(pm, (w[o >> 2] >> (8 * (o & 3))) & 0xffu);
+#pragma unroll
+                for (int o = 0; o < 13; ++o)
+                    if (o >= ro && o <= oo) w[o >> 2] -= pm << (8 * (o & 3));
+                /* byte 14: some delta >= 16 (v_pk_lshrrev_b16 shifts by the amount mod 16, so such
+                 * a row takes the 32-bit path) */
+                uint32_t dmax = 0;
+#pragma unroll
+                for (int o = 0; o < 13; ++o)
+                    if (o >= ro && o <= oo) dmax = max(dmax, (w[o >> 2] >> (8 * (o & 3))) & 0xffu);
+                w[3] = (w[3] & 0x0000ffffu) | ((dmax >= 16 ? 1u : 0u) << 16) | (pm << 24);
+                r[0] = w[0], r[1] = w[1], r[2] = w[2], r[3] = w[3];
+            }
+            __syncthreads();
             const uint4* pkv = reinterpret_cast<const uint4*>(hs);
             uint64_t tb[16];
+            uint32_t tp[16]; /* packed-path totals: this thread's sum(y >> d) < 4 * 8 * 2^16 per order */
 #pragma unroll
-            for (int o = 0; o < 16; ++o) tb[o] = 0;
+            for (int o = 0; o < 16; ++o) tb[o] = 0, tp[o] = 0;
             for (int c = tid; c < nch; c += NT) {
                 const uint4 u = reinterpret_cast<const uint4*>(zz)[2 * c], v = reinterpret_cast<const uint4*>(zz)[2 * c + 1];
                 const uint32_t z[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
                 const uint4 pv = pkv[c / cpp];
-                if (((u.x | u.y | u.z | u.w | v.x | v.y | v.z | v.w) >> 29) == 0) {
+                const uint32_t pm = pv.w >> 24;
+                uint32_t y[8], yo = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) y[k] = z[k] >> pm, yo |= y[k];
+                if ((yo >> 16) == 0 && ((pv.w >> 16) & 0xffu) == 0) { /* tp < chunks per thread * 8 * 2^16 < 2^32 */
+                    uint32_t yp[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) yp[i] = __builtin_amdgcn_perm(y[2 * i + 1], y[2 * i], 0x05040100u);
+                    const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+                    for (int o = 0; o < 16; ++o)
+                        if (o >= ro && o <= oo) {
+                            /* d = p_o - pm in both halves */
+                            const uint32_t sel = (o & 3) == 0 ? 0x0c000c00u : (o & 3) == 1 ? 0x0c010c01u
+                                                 : (o & 3) == 2 ? 0x0c020c02u : 0x0c030c03u;
+                            const us2x d = __builtin_bit_cast(us2x, __builtin_amdgcn_perm(0u, pw[o >> 2], sel));
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+                                tp[o] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2x, yp[i]) >> d, us2x{1, 1}, tp[o], false);
+                        }
+                } else if (((u.x | u.y | u.z | u.w | v.x | v.y | v.z | v.w) >> 29) == 0) {
+                    const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w + 0u};
+                    (void)pw;
                     uint32_t t32[16];
 #pragma unroll
                     for (int o = 0; o < 16; ++o) t32[o] = 0;
-                    chunk_rice_bits(z, pv, ro, oo, t32);
+                    chunk_rice_bits(y, pv, ro, oo, t32); /* deltas applied to y = z >> pm */
 #pragma unroll
                     for (int o = 0; o < 16; ++o)
                         if (o >= ro && o <= oo) tb[o] += t32[o];
@@ -1893,12 +1947,14 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
 #pragma unroll
                     for (int o = 0; o < 16; ++o)
                         if (o >= ro && o <= oo) {
-                            const uint32_t p = (pw[o >> 2] >> (8 * (o & 3))) & 0xffu;
+                            const uint32_t d = (pw[o >> 2] >> (8 * (o & 3))) & 0xffu;
 #pragma unroll
-                            for (int k = 0; k < 8; ++k) tb[o] += (uint64_t)(z[k] >> p);
+                            for (int k = 0; k < 8; ++k) tb[o] += (uint64_t)(y[k] >> d);
                         }
                 }
             }
+#pragma unroll
+            for (int o = 0; o < 16; ++o) tb[o] += tp[o];
 #pragma unroll
             for (int o = 0; o < 16; ++o)
                 if (o >= ro && o <= oo) {
@@ -1929,7 +1985,10 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             __syncthreads();
             const int best = misc[3];
             int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
-            for (int K = tid; K < (1 << best); K += NT) rp[K] = pk[16 * (K << (omax - best)) + best];
+            for (int K = tid; K < (1 << best); K += NT) {
+                const int row = 16 * (K << (omax - best));
+                rp[K] = pk[row + 15] + pk[row + best]; /* pm + delta */
+            }
             return;
         }
     }

@@ -68,7 +68,7 @@ struct SLds {
 /* Workgroup LDS (bytes).  Regions whose lifetimes do not overlap share space, which keeps a
  * config-2 unit (n = 4608, two waves) at 10160 B: 16 workgroups per CU.
  *   xs   biased samples behind a 16-sample zero pad             staging .. Rice recompute
- *   pk   u32 [P][RS] Rice parameters p | p << 16 per order       Rice (after B3)
+ *   pk   u16 [P][RS] Rice parameters per order (entry 0 bit 15: flag) Rice (after B3)
  *   rec  the LPC orders' f16 tap table (aliases pk, tap_table)  staging .. MFMA operands
  *   red  u64 [nw][group][order] MFMA partial sums               MFMA phase .. choice
  *   red2 u64 [nw + 1][order] data bits (aliases red)            Rice (after B3)
@@ -80,7 +80,7 @@ __host__ __device__ inline SLds stream_lds(int n, int nw, int tap_words, int P, 
     SLds l;
     int o = 0;
     l.xs = o;   o = up(o + 2 * (kSHP + n));
-    l.pk = l.rec = o; o = up(o + mx(4 * P * RS, 4 * mx(tap_words, 1)));
+    l.pk = l.rec = o; o = up(o + mx(2 * P * RS, 4 * mx(tap_words, 1)));
     l.red = l.red2 = o; o = up(o + mx(8 * nw * 16, 8 * (nw + 1) * kRiceOrders));
     l.red0 = o; o = up(o + 4 * nw);
     l.pks = o;  o = up(o + 4 * P);
@@ -191,12 +191,20 @@ __device__ __forceinline__ int rice_param_exact(uint64_t s, int len) {
     return p;
 }
 
-/* one finest partition's Rice table row (32 bytes: p | p << 16 per order) */
-__device__ __forceinline__ void load_ptab(const uint32_t* row, uint32_t (&pv)[kRiceOrders]) {
+/* one finest partition's Rice table row (16 bytes: a u16 parameter per order); word o / 2
+ * holds orders o (low half) and o + 1 (high half) */
+__device__ __forceinline__ void load_ptab(const uint16_t* row, uint32_t (&w)[kRiceOrders / 2]) {
     const uint4 a = *reinterpret_cast<const uint4*>(row);
-    const uint4 b = *reinterpret_cast<const uint4*>(row + 4);
-    pv[0] = a.x, pv[1] = a.y, pv[2] = a.z, pv[3] = a.w;
-    pv[4] = b.x, pv[5] = b.y, pv[6] = b.z, pv[7] = b.w;
+    w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w;
+}
+/* both halves of the 16-bit pair d shifted right by the low (HI = 0) or high (HI = 1) half
+ * of s: op_sel broadcasts that half to both lanes (no splat instruction) */
+template <int HI>
+__device__ __forceinline__ uint32_t pk_shr_bcast(uint32_t s, uint32_t d) {
+    uint32_t r;
+    if constexpr (HI) asm("v_pk_lshrrev_b16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(s), "v"(d));
+    else asm("v_pk_lshrrev_b16 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(s), "v"(d));
+    return r;
 }
 
 /* fixed order K residual of samples i0..i0+7 from biased LDS samples, zig-zagged; the
@@ -311,14 +319,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (n % (1 << o) == 0) rmax_eff = o;
     const int Pmax = 1 << rmax_eff; /* host-checked: 0 <= rmax_eff <= 5 */
-    constexpr int RS = kRiceOrders; /* Rice table words per finest partition (32-byte rows) */
+    constexpr int RS = kRiceOrders; /* Rice table entries per finest partition (16-byte rows: at
+                                     * 10160 B a config-2 unit keeps 16 workgroups per CU) */
     const SLds lay = stream_lds(n, nw, tap_table_words(NG), Pmax, RS);
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem + lay.xs) + kSHP;
     int32_t* recl = reinterpret_cast<int32_t*>(smem + lay.rec);
     uint32_t* red0 = reinterpret_cast<uint32_t*>(smem + lay.red0);
     unsigned long long* red2 = reinterpret_cast<unsigned long long*>(smem + lay.red2);
     uint32_t* pks = reinterpret_cast<uint32_t*>(smem + lay.pks); /* finest partition sums */
-    uint32_t* pkw = reinterpret_cast<uint32_t*>(smem + lay.pk);
+    uint16_t* pkw = reinterpret_cast<uint16_t*>(smem + lay.pk);
     flacmi_unit_meta* meta = a.meta + gid;
     MetaVals mv{};
 
@@ -825,13 +834,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     }
     /* this wave's table: finest partition k (lane k) -> the parameter of its ancestor at
      * every order, as p | p << 16 */
+    int pmax = 0;
+    /* (opaque: lane * 16 bytes would otherwise be shared with the staging's kFixB offset and
+     * held, or spilled, across the whole kernel) */
+    uint16_t* const prow = pkw + (int)opaque((uint32_t)lane) * RS;
 #pragma unroll
     for (int o2 = 0; o2 < kRiceOrders; ++o2) {
         if (o2 >= ro && o2 <= oo) {
             const int node = (1 << o2) + (lane >> (oo - o2));
             const int pv = __shfl(prm, (node - 1) & 63);
-            if (lane < P) pkw[lane * RS + o2] = (uint32_t)pv * 0x10001u;
+            pmax = max(pmax, pv);
+            if (lane < P) prow[o2] = (uint16_t)pv;
         }
+    }
+    /* bit 15 of a row's entry 0 (order 0's parameter, or unused when rmin > 0): some order's
+     * parameter is >= 16, which v_pk_lshrrev_b16 would take mod 16, so the row's chunks take
+     * the 32-bit path (possible only where a partition's mean is >= 2^16 while one of its
+     * chunks stays below 2^16) */
+    if (lane < P) {
+        if (ro > 0) prow[0] = pmax >= 16 ? 0x8000u : 0u;
+        else if (pmax >= 16) prow[0] |= 0x8000u;
     }
     __builtin_amdgcn_wave_barrier();
     /* data bits: sum of x >> p over the residual for every candidate order */
@@ -843,17 +865,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         const int c = tid + jc * NT;
         if (c < nch) {
             const int k = part_of(c);
-            uint32_t pv[kRiceOrders]; /* p | p << 16 per order */
-            load_ptab(pkw + k * RS, pv);
+            uint32_t pw[kRiceOrders / 2];
+            load_ptab(pkw + k * RS, pw);
+            big |= ((pw[0] >> 15) & 1u) << jc; /* a parameter >= 16 in this chunk's row */
             if (!((big >> jc) & 1)) {
 #pragma unroll
                 for (int o2 = 0; o2 < kRiceOrders; ++o2)
                     if (o2 >= ro && o2 <= oo) {
-                        const us2 sv = __builtin_bit_cast(us2, pv[o2]);
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            tb[o2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, zp[jc][i]) >> sv, us2{1, 1}, tb[o2],
-                                                            false);
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t sh = (o2 & 1) ? pk_shr_bcast<1>(pw[o2 >> 1], zp[jc][i])
+                                                         : pk_shr_bcast<0>(pw[o2 >> 1], zp[jc][i]);
+                            tb[o2] = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, sh), us2{1, 1}, tb[o2], false);
+                        }
                     }
             }
         }
@@ -867,14 +891,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             if (!((big >> jc) & 1)) continue;
             const int c = tid + jc * NT;
             const int k = part_of(c);
-            uint32_t pw[kRiceOrders];
+            uint32_t pw[kRiceOrders / 2];
             load_ptab(pkw + k * RS, pw);
             uint32_t z[8];
             resid(c, z);
 #pragma unroll
             for (int o2 = 0; o2 < kRiceOrders; ++o2)
                 if (o2 >= ro && o2 <= oo) {
-                    const uint32_t sh = pw[o2] & 0xffffu;
+                    const uint32_t sh = (pw[o2 >> 1] >> (16 * (o2 & 1))) & 0x7fffu;
                     tb[o2] += (z[0] >> sh) + (z[1] >> sh) + (z[2] >> sh) + (z[3] >> sh) + (z[4] >> sh) +
                               (z[5] >> sh) + (z[6] >> sh) + (z[7] >> sh);
                 }
@@ -973,7 +997,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     }
 #endif
     int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
-    if (lane < (1 << best)) rp[lane] = (int32_t)(pkw[(lane << (oo - best)) * RS + best] & 0xffffu);
+    if (lane < (1 << best)) rp[lane] = (int32_t)(pkw[(lane << (oo - best)) * RS + best] & 0x7fffu);
 }
 
 /* units the stream kernel listed (outside its MFMA bound) are handled by k_resid's list

@@ -400,6 +400,28 @@ def test_wide_rice_wave0_parameters_and_errors(az, n, rmax):
     assert len(sts) >= 2, sts
 
 
+def test_stream_rice_parameters_of_16_and_more(az):
+    """k_resid_stream's packed Rice pass shifts 16-bit pairs by the parameter, which
+    v_pk_lshrrev_b16 takes mod 16: a finest partition whose mean is >= 2^16 (parameter >= 16)
+    while some of its chunks stay below 2^16 must take the 32-bit path.  Loud smooth sines
+    (fixed order 1 wins) with full-scale alternation in 10..14 chunks of one finest partition:
+    that partition's parameter is 16, and the oracle picks the 32 finest partitions."""
+    n, units = 4608, 8
+    r = np.random.default_rng(7)
+    a = np.zeros((units, n), np.int16)
+    t = np.arange(n)
+    for u in range(units):
+        x = (20000 + 1000 * u) * np.sin(2 * np.pi * t / (900 + 37 * u) + u) + r.normal(0, 3, n)
+        k = 5 + 3 * u
+        for c in range(10 + u % 5):
+            x[144 * k + 8 * c: 144 * k + 8 * c + 8] = 32767 * np.array([1, -1] * 4)
+        a[u] = np.clip(np.round(x), -32768, 32767)
+    out = az.analyze(a, make_params(12, 5, 0, 5), n, sample_bits=16, debug=True)
+    ora = oracle.analyze_batch(a, oracle.make_params(12, 5, 0, 5), n, sample_bits=16, threads=16)
+    assert set(int(v) for v in ora["meta"]["part_order"]) == {5}
+    compare_with_oracle(out, ora, [n] * units)
+
+
 @pytest.mark.parametrize("rmin,rmax", [(0, 6), (3, 2)])
 def test_fast_kernel_stages_the_whole_record(az, rmin, rmax):
     """The S16 fast kernel with a 64-thread workgroup (n = 1024) and L = 12: the LPC record
