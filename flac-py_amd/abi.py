@@ -191,6 +191,8 @@ DSITE = {name: 32 + i for i, name in enumerate((
     "samples"))}
 
 
+COMM_ID_BYTES = 128  # FLACMI_COMM_ID_BYTES
+
 # Every symbol include/flacmi.h declares, with its ctypes signature.
 SIGNATURES = {
     "flacmi_abi_version": (C.c_int, []),
@@ -222,6 +224,10 @@ SIGNATURES = {
                                               C.c_void_p, C.c_void_p, C.c_void_p]),
     "flacmi_stream_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
                                       C.c_int64, C.c_void_p, C.c_void_p]),
+    "flacmi_comm_id": (C.c_int, [C.c_void_p]),
+    "flacmi_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
+    "flacmi_allreduce_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "flacmi_comm_destroy": (C.c_int, [C.c_void_p]),
     "flacmi_synth_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,
                                       C.c_int64, C.c_int64, C.c_int32, C.c_uint64, C.c_void_p]),
     "flacmi_device_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),

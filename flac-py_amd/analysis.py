@@ -358,6 +358,36 @@ class Analyzer:
                                            n_tail_units, stats_ptr, stream), "flacmi_stream_stats")
 
 
+class StatsComm:
+    """The cross-GPU stream-statistics reduce of the C-ABI (flacmi_comm_* /
+    flacmi_allreduce_stats: RCCL over xGMI), for callers without torch.distributed.  Rank 0
+    calls comm_id() and hands the bytes to every rank; every rank builds StatsComm(az,
+    nranks, rank, id) (a collective call)."""
+
+    def __init__(self, az: "Analyzer", nranks: int, rank: int, comm_id: bytes):
+        if len(comm_id) != abi.COMM_ID_BYTES:
+            raise ValueError(f"comm id must be {abi.COMM_ID_BYTES} bytes")
+        self.lib = az.lib
+        buf = C.create_string_buffer(bytes(comm_id), abi.COMM_ID_BYTES)
+        h = C.c_void_p()
+        check(self.lib.flacmi_comm_init(az.ctx, nranks, rank, buf, C.byref(h)), "flacmi_comm_init")
+        self.comm = h.value
+
+    @staticmethod
+    def comm_id(lib) -> bytes:
+        buf = C.create_string_buffer(abi.COMM_ID_BYTES)
+        check(lib.flacmi_comm_id(buf), "flacmi_comm_id")
+        return buf.raw
+
+    def allreduce_stats(self, stats_ptr: int, stream: int = 0) -> None:
+        check(self.lib.flacmi_allreduce_stats(self.comm, stats_ptr, stream), "flacmi_allreduce_stats")
+
+    def close(self) -> None:
+        if self.comm:
+            check(self.lib.flacmi_comm_destroy(self.comm), "flacmi_comm_destroy")
+            self.comm = None
+
+
 def unit_result(out: dict, i: int) -> dict:
     """Per-unit dict view of analyze() results (the keys tests/golden_util.check reads)."""
     m = out["meta"][i]

@@ -11,6 +11,7 @@
  *   - the int16 sine table of the synthetic generator (libm sin).
  * This file is compiled with -ffp-contract=off like the kernels.
  */
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1217,6 +1218,96 @@ int flacmi_stream_stats(flacmi_ctx* ctx, const flacmi_unit_meta* d_meta, int64_t
     HIP_TRY(hipMemsetAsync(d_stats, 0, sizeof(int64_t) * FLACMI_STATS_WORDS, (hipStream_t)stream));
     HIP_TRY(launch_stats(d_meta, n_units, block_len, tail_len, n_tail_units, d_stats, (hipStream_t)stream));
     return 0;
+}
+
+/* ---- RCCL stats reduce: librccl.so.1 is opened on first use (no link-time dependency, so
+ * the product library loads where RCCL is absent; a process that already loaded RCCL, e.g.
+ * through torch, gets the same library back from dlopen) ---- */
+namespace {
+struct Rccl {
+    void* h = nullptr;
+    int (*get_id)(void* id) = nullptr;
+    int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+    int (*destroy)(void*) = nullptr;
+    const char* (*err)(int) = nullptr;
+};
+struct RcclId {
+    char b[FLACMI_COMM_ID_BYTES];
+};
+/* ncclCommInitRank takes the 128-byte ncclUniqueId by value */
+typedef int (*rccl_init_rank_t)(void** comm, int nranks, RcclId id, int rank);
+Rccl g_rccl;
+rccl_init_rank_t g_rccl_init = nullptr;
+std::mutex g_rccl_mu;
+constexpr int kNcclInt64 = 4, kNcclSum = 0; /* ncclDataType_t ncclInt64, ncclRedOp_t ncclSum */
+
+int rccl_load() {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (g_rccl.h) return 0;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return fail(FLACMI_E_UNSUPPORTED, "librccl.so.1 not found: %s", dlerror());
+    Rccl r;
+    r.h = h;
+    r.get_id = (int (*)(void*))dlsym(h, "ncclGetUniqueId");
+    g_rccl_init = (rccl_init_rank_t)dlsym(h, "ncclCommInitRank");
+    r.all_reduce = (int (*)(const void*, void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclAllReduce");
+    r.destroy = (int (*)(void*))dlsym(h, "ncclCommDestroy");
+    r.err = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
+    if (!r.get_id || !g_rccl_init || !r.all_reduce || !r.destroy || !r.err)
+        return fail(FLACMI_E_UNSUPPORTED, "librccl.so.1 lacks an entry point");
+    g_rccl = r;
+    return 0;
+}
+int rccl_fail(const char* what, int rc) {
+    return fail(FLACMI_E_HIP, "%s: RCCL error %d (%s)", what, rc, g_rccl.err ? g_rccl.err(rc) : "?");
+}
+}  // namespace
+
+struct flacmi_comm {
+    flacmi_ctx* ctx;
+    void* comm; /* ncclComm_t */
+    int nranks, rank;
+};
+
+int flacmi_comm_id(void* id_out) {
+    if (!id_out) return fail(FLACMI_E_INVALID, "null argument");
+    if (int rc = rccl_load()) return rc;
+    if (int rc = g_rccl.get_id(id_out)) return rccl_fail("ncclGetUniqueId", rc);
+    return 0;
+}
+
+int flacmi_comm_init(flacmi_ctx* ctx, int nranks, int rank, const void* id, flacmi_comm** out) {
+    if (!ctx || !id || !out) return fail(FLACMI_E_INVALID, "null argument");
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(FLACMI_E_INVALID, "rank %d of %d", rank, nranks);
+    if (int rc = rccl_load()) return rc;
+    if (int rc = set_device(ctx)) return rc;
+    RcclId cid;
+    memcpy(cid.b, id, FLACMI_COMM_ID_BYTES);
+    void* c = nullptr;
+    if (int rc = g_rccl_init(&c, nranks, cid, rank)) return rccl_fail("ncclCommInitRank", rc);
+    *out = new flacmi_comm{ctx, c, nranks, rank};
+    return 0;
+}
+
+int flacmi_allreduce_stats(flacmi_comm* comm, int64_t* d_stats, void* stream) {
+    if (!comm || !d_stats) return fail(FLACMI_E_INVALID, "null argument");
+    if (int rc = set_device(comm->ctx)) return rc;
+    if (int rc = g_rccl.all_reduce(d_stats, d_stats, FLACMI_STATS_WORDS, kNcclInt64, kNcclSum, comm->comm,
+                                   (hipStream_t)stream))
+        return rccl_fail("ncclAllReduce", rc);
+    return 0;
+}
+
+int flacmi_comm_destroy(flacmi_comm* comm) {
+    if (!comm) return 0;
+    int rc = 0;
+    if (comm->comm && g_rccl.destroy) {
+        if (int e = g_rccl.destroy(comm->comm)) rc = rccl_fail("ncclCommDestroy", e);
+    }
+    delete comm;
+    return rc;
 }
 
 int flacmi_synth_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_t sample_bits, int64_t unit_stride,

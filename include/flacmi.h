@@ -375,6 +375,22 @@ int flacmi_stream_stats(flacmi_ctx* ctx, const flacmi_unit_meta* d_meta, int64_t
                         int32_t block_len, int32_t tail_len, int64_t n_tail_units,
                         int64_t* d_stats, void* stream);
 
+/* ---- the cross-GPU stats reduce without torch (SURVEY §8b flacmi_allreduce_stats) ----- */
+/* One process (or host thread) per GPU.  Rank 0 makes an id with flacmi_comm_id and hands
+ * its FLACMI_COMM_ID_BYTES to every rank over any out-of-band channel (a file, a socket,
+ * MPI); each rank then calls flacmi_comm_init with the same id, the world size and its rank
+ * (collective: every rank must call it).  RCCL (librccl.so.1, loaded on first use) runs
+ * the all-reduce over xGMI.  Replaces the reference's nothing: flac-py is single-process;
+ * the streams' statistics are the only cross-GPU exchange (encoder.py:81 writes no MD5). */
+#define FLACMI_COMM_ID_BYTES 128
+typedef struct flacmi_comm flacmi_comm;
+int flacmi_comm_id(void* id_out);
+int flacmi_comm_init(flacmi_ctx* ctx, int nranks, int rank, const void* id, flacmi_comm** out);
+/* Sum of every rank's FLACMI_STATS_WORDS int64 words, in place (device pointer), enqueued
+ * on `stream` (a stream of the communicator's context device). */
+int flacmi_allreduce_stats(flacmi_comm* comm, int64_t* d_stats, void* stream);
+int flacmi_comm_destroy(flacmi_comm* comm);
+
 /* ---- synthetic PCM (BASELINE configs 2-5) --------------------------------- */
 /* Writes units [first_unit, first_unit + n_units) of the integer synthetic signal into
  * dst[(u - first_unit) * unit_stride ...]: sum of 3 DDS sinusoids + splitmix64 noise,
