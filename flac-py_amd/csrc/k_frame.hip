@@ -627,6 +627,8 @@ __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
  * starts at 0), shifts it to E with the x^(8*2^b) tables and the workgroup XORs the
  * shares.  The frame is stored with 16-byte stores (dword / byte stores at its two ends).
  * ==================================================================================== */
+template <int MAXC> /* chunks per thread the launch guarantees (2..kMaxC): fewer registers, more
+                     * frames in flight per CU */
 __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
     __shared__ uint32_t win[kWinWords];
     __shared__ uint16_t ct[4 * 256];
@@ -733,11 +735,11 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
         const int nch = (n + 7) >> 3;
         const int cpt = (nch + NT - 1) / NT;
         const int k0 = tid * cpt, k1 = min(k0 + cpt, nch);
-        uint32_t z[kMaxC][8];
-        int pa[kMaxC], pb[kMaxC], bnd[kMaxC], pt0[kMaxC];
+        uint32_t z[MAXC][8];
+        int pa[MAXC], pb[MAXC], bnd[MAXC], pt0[MAXC];
         uint32_t tsum = 0;
 #pragma unroll
-        for (int j = 0; j < kMaxC; ++j) {
+        for (int j = 0; j < MAXC; ++j) {
             const int k = k0 + j;
             const int i0 = 8 * k;
             pa[j] = pb[j] = 0;
@@ -796,7 +798,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
         };
         const uint32_t pmask_m = (1u << method) - 1u;
 #pragma unroll
-        for (int j = 0; j < kMaxC; ++j) {
+        for (int j = 0; j < MAXC; ++j) {
             const int k = k0 + j;
             if (k < k1 && !(a.ablate & 2)) {
                 const int i0 = 8 * k;
@@ -940,7 +942,10 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     if (b.pack_split) {
         hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
         if (e0 != hipSuccess) return e0;
-        hipLaunchKernelGGL(k_pack32, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
+        const int cpt = (nch + nt - 1) / nt;
+        if (cpt <= 2) hipLaunchKernelGGL(k_pack32<2>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
+        else if (cpt == 3) hipLaunchKernelGGL(k_pack32<3>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
+        else hipLaunchKernelGGL(k_pack32<kMaxC>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
