@@ -1053,16 +1053,23 @@ __device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta
  *   kVarFast     unit = blockIdx.x, only the S16 MFMA path with a register-resident
  *                residual (smaller register footprint: more workgroups per CU); a unit
  *                outside the MFMA exactness bound is marked FLACMI_STATUS_RETRY and listed;
- *   kVarList     unit = retry_list[blockIdx.x] for blockIdx.x < *retry_count, every path. */
+ *   kVarList     units retry_list[li], li = blockIdx.x, blockIdx.x + gridDim.x, ... below
+ *                *retry_count, every path. */
 enum { kVarGeneric = 0, kVarFast = 1, kVarList = 2 };
 template <int LMAX, int PATH, typename ResT, int VAR>
 __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArgs a) {
     constexpr bool FAST = VAR == kVarFast;
-    int64_t gid = blockIdx.x;
+    /* the list variant (units another kernel handed over) loops over the list with a small
+     * grid (kListGrid) instead of a workgroup per unit of the batch: a million near-empty
+     * workgroups cost ~0.3 ms of dispatch at config 2.  Every exit of the body is
+     * workgroup-uniform, so each one goes to the next listed unit. */
+    int64_t li = blockIdx.x, gid = blockIdx.x;
     if constexpr (VAR == kVarList) {
-        if (gid >= (int64_t)*a.retry_count) return;
-        gid = a.retry_list[gid];
+        if (li >= (int64_t)*a.retry_count) return;
     }
+next_unit:
+    if constexpr (VAR == kVarList) gid = a.retry_list[li];
+    {
     using UX = ResT;
     constexpr bool S16 = PATH == PATH_S16;
     constexpr bool WIDE = PATH == PATH_W64 || PATH == PATH_W64S;
@@ -1159,7 +1166,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
         const int st = recl[0];
         if (st != 0) { /* the reference raises inside encode_subframe_lpc */
             if (tid == 0) put_meta(meta, st & 0xffff, st >> 16, nullptr, 0);
-            return;
+            goto unit_done;
         }
         const uint32_t negmask = (uint32_t)recl[1];
         for (int i = tid; i < LMAX * CT::CPAD; i += NT) {
@@ -1312,7 +1319,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     }
     if (st_rec != 0) { /* the reference raises inside encode_subframe_lpc */
         if (tid == 0) put_meta(meta, st_rec & 0xffff, st_rec >> 16, nullptr, 0);
-        return;
+        goto unit_done;
     }
     if (do_lpc) {
         const uint32_t negmask = (uint32_t)rec[1];
@@ -1430,7 +1437,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             }
         }
     }
-    if (a.stop_after == 1) return;
+    if (a.stop_after == 1) goto unit_done;
 
     /* ---- phase B: sum|r| for fixed orders 0..4 and LPC orders 1..L ---- */
     if (FAST && !use_mfma) { /* outside the MFMA exactness bound: the generic kernel redoes it */
@@ -1439,18 +1446,18 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             const unsigned long long k = atomicAdd(a.retry_count, 1ull);
             a.retry_list[k] = gid;
         }
-        return;
+        goto unit_done;
     }
     if (use_mfma) {
         if constexpr (MF)
             mfma_candidate_sums<LMAX>(xs16, reinterpret_cast<const float*>(smem + lay.coef + CT::TAPF_OFF), lsh, L,
                                       n, lane, wid, nw, red, sumx);
-        if (a.stop_after == 2) return;
+        if (a.stop_after == 2) goto unit_done;
     } else if (MF8 && use_mf8) {
         if constexpr (MF8)
             lpc_pruned = mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
                                                   nw, red, a.prune != 0 && !lpc_only && !rice_only);
-        if (a.stop_after == 2) return;
+        if (a.stop_after == 2) goto unit_done;
     } else if constexpr (!FAST) {
     A acc[NSUM];
 #pragma unroll
@@ -1480,7 +1487,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
 
     if (a.stop_after == 2) {
         if (tid == 0) meta->rice_bits = (long long)acc[0] + (long long)acc[NSUM - 1];
-        return;
+        goto unit_done;
     }
     /* ---- phase C: workgroup reduction ---- */
     {
@@ -1599,9 +1606,9 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     const int dstatus = dec->status;
     if (dstatus != ST_OK) {
         if (tid == 0) put_meta(meta, dstatus, dec->site, dec, 0);
-        return;
+        goto unit_done;
     }
-    if (a.stop_after == 3) return;
+    if (a.stop_after == 3) goto unit_done;
     const int order = dec->order;
     const int dshift = dec->shift;
     /* the residual starts at index len(warmup); a coefficient-less LPC subframe (only
@@ -1735,16 +1742,16 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 }
             }
             __syncthreads();
-            if (a.stop_after == 4) return;
+            if (a.stop_after == 4) goto unit_done;
             if (lpc_only) {
                 lpc_only_done();
-                return;
+                goto unit_done;
             }
             /* ---- phase F (register-resident) ---- */
             const int omax = first_order();
             if (omax < 0) {
                 if (tid == 0) put_meta(meta, ST_ASSERT, FLACMI_SITE_RICE_NO_ORDER, dec, 1);
-                return;
+                goto unit_done;
             }
             const int cpp = (n >> omax) >> 3; /* chunks per finest partition */
             uint8_t* pk = reinterpret_cast<uint8_t*>(hs);
@@ -1760,7 +1767,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             __syncthreads();
             if (misc[0] >= 0) {
                 if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
-                return;
+                goto unit_done;
             }
             const int ro = __builtin_amdgcn_readfirstlane(a.rmin), oo = __builtin_amdgcn_readfirstlane(omax);
             uint32_t tb[16];
@@ -1772,7 +1779,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 if (c < nch) chunk_rice_bits(zr[j], *reinterpret_cast<const uint4*>(pk + 16 * (c / cpp)), ro, oo, tb);
             }
             rice_finish(a, meta, dec, tb, rb, red, misc, pk, n, start, a.rmin, omax, tid, NT, lane, wid, nw, gid);
-            return;
+            goto unit_done;
         }
     }
     if constexpr (!FAST) {
@@ -1810,21 +1817,21 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     }
     if (wide_flag) misc[2] = 1;
     __syncthreads();
-    if (a.stop_after == 4) return;
+    if (a.stop_after == 4) goto unit_done;
     if (misc[2]) {
         if (tid == 0) put_meta(meta, FLACMI_STATUS_RESIDUAL_WIDE, FLACMI_SITE_RESIDUAL_WIDTH, dec, 1);
-        return;
+        goto unit_done;
     }
     if (a.mode == FLACMI_MODE_LPC_ONLY) {
         lpc_only_done();
-        return;
+        goto unit_done;
     }
 
     /* ---- phase F: Rice partition search (encoder.py:655-760) ---- */
     const int omax = first_order();
     if (omax < 0) {
         if (tid == 0) put_meta(meta, ST_ASSERT, FLACMI_SITE_RICE_NO_ORDER, dec, 1);
-        return;
+        goto unit_done;
     }
     const int rmin = a.rmin;
     const int P = 1 << omax, ps = n >> omax;
@@ -1847,7 +1854,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             __syncthreads();
             if (misc[0] >= 0) {
                 if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
-                return;
+                goto unit_done;
             }
             const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
             uint32_t tb[16];
@@ -1859,7 +1866,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 chunk_rice_bits(z, *reinterpret_cast<const uint4*>(pk + 16 * (c / cpp)), ro, oo, tb);
             }
             rice_finish(a, meta, dec, tb, rb, red, misc, pk, n, start, rmin, omax, tid, NT, lane, wid, nw, gid);
-            return;
+            goto unit_done;
         }
     }
     if constexpr (WIDE && sizeof(ResT) == 4) {
@@ -1875,7 +1882,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             __syncthreads();
             if (misc[0] >= 0) {
                 if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
-                return;
+                goto unit_done;
             }
             const int cpp = ps >> 3;
             const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
@@ -1989,7 +1996,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
                 const int row = 16 * (K << (omax - best));
                 rp[K] = pk[row + 15] + pk[row + best]; /* pm + delta */
             }
-            return;
+            goto unit_done;
         }
     }
     /* finest partition sums: heap nodes [P, 2P); zz[i] = 0 for i < start */
@@ -2035,7 +2042,7 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
             put_meta(meta, ST_VALUE,
                      hs[(1 << o) + K] == 0 ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT, dec, 1);
         }
-        return;
+        goto unit_done;
     }
     /* data bits: sum over the residual of (x >> p) for every candidate order at once */
     uint64_t tb[16];
@@ -2129,6 +2136,15 @@ __global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArg
     int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
     for (int K = tid; K < (1 << best); K += NT) rp[K] = hp[(1 << best) + K];
     } /* !FAST */
+    }
+unit_done:
+    if constexpr (VAR == kVarList) {
+        li += gridDim.x;
+        if (li < (int64_t)*a.retry_count) {
+            __syncthreads(); /* every wave is done with this unit's LDS */
+            goto next_unit;
+        }
+    }
 }
 
 
@@ -2149,6 +2165,8 @@ static hipError_t launch_resid_T(const ResidArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+constexpr int kListGrid = 2048; /* workgroups of a list launch (each loops over the list) */
+
 /* S16 MFMA fast kernel over the batch, then the generic body over the units it listed */
 template <int LMAX>
 static hipError_t launch_resid_fast(const ResidArgs& a, hipStream_t s) {
@@ -2168,11 +2186,11 @@ static hipError_t launch_resid_fast(const ResidArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(kf, dim3((unsigned)a.count), dim3(nt), lds_fast, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_poison_lds(s)) != hipSuccess) return e;
-    /* the listed units: one workgroup each; the rest of the grid exits on the count */
+    /* the listed units: a small grid loops over the list */
     auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
     e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_gen);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kl, dim3((unsigned)a.count), dim3(nt), lds_gen, s, a);
+    hipLaunchKernelGGL(kl, dim3((unsigned)(a.count < kListGrid ? a.count : kListGrid)), dim3(nt), lds_gen, s, a);
     return hipGetLastError();
 }
 
@@ -2191,7 +2209,7 @@ static hipError_t launch_resid_list(const ResidArgs& a, hipStream_t s) {
     auto kl = k_resid<LMAX, PATH_S16, uint32_t, kVarList>;
     hipError_t e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kl, dim3((unsigned)a.count), dim3(nt), lds, s, a);
+    hipLaunchKernelGGL(kl, dim3((unsigned)(a.count < kListGrid ? a.count : kListGrid)), dim3(nt), lds, s, a);
     return hipGetLastError();
 }
 
