@@ -551,3 +551,23 @@ def test_lpc_pruning_paths_vs_oracle(az, q):
         assert pruned[:24].sum() >= 12, "config-2 units should mostly prune"
     assert (ok & ~pruned & (om["kind"] == abi.KIND_FIXED)).any(), "no unit took the exact pass and chose fixed"
     assert (ok & (om["kind"] == abi.KIND_LPC)).any(), "no LPC-chosen unit"
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_production_batches_vs_oracle(az, cfg):
+    """Production calls (no debug outputs: LPC pruning on, every kernel variant the dispatch
+    picks) over larger batches of the bench's own synthetic units against the oracle: 2048
+    config-2 units (k_resid_stream, its retry list) and 192 config-3 units (k_resid's int8-MFMA
+    path with eighth tiers and the packed Rice pass).  A unit reporting FLACMI_LPC_PRUNED must
+    lose to fixed in the oracle; every other field is compared bit for bit."""
+    if cfg == "c2":
+        n, bits, L, q, rmax, units, dt = 4608, 16, 12, 5, 5, 2048, np.int16
+    else:
+        n, bits, L, q, rmax, units, dt = 16384, 24, 32, 15, 8, 192, np.int32
+    a = oracle.synth_batch(5000, units, n, bits, 11, dtype=dt)
+    out = az.analyze(a, make_params(L, q, 0, rmax), n, sample_bits=bits)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, rmax), n, sample_bits=bits, threads=16)
+    compare_with_oracle(out, ora, [n] * units)
+    pruned = out["meta"]["lpc_order"] == abi.LPC_PRUNED
+    assert pruned.mean() > 0.9, pruned.mean()
+    assert (ora["meta"]["kind"][pruned] == abi.KIND_FIXED).all()
