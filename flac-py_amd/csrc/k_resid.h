@@ -818,6 +818,33 @@ __device__ __forceinline__ void fixed_resid_chunk(const int16_t* xs16, int i0, u
     }
 }
 
+/* Phase E for a fixed predictor of order K on 32-bit LDS samples with |x| <= 2^23 (the
+ * int8-MFMA path's digit check): the K-th difference (encoder.py:331-359) stays below 2^27,
+ * so the chain runs in int32 instead of K 64-bit multiply-adds per value.  Values i < K and
+ * i >= n give 0 (only the first and a ragged last chunk test them). */
+template <int K, typename ResT>
+__device__ __forceinline__ void fixed_resid_chunk32(const int32_t* xs32, int i0, int n, ResT (&zv)[8]) {
+    int32_t d[12]; /* samples i0-4 .. i0+7 (history pad >= 4) */
+    const int4v* src = reinterpret_cast<const int4v*>(xs32 + i0 - 4);
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        const int4v v = src[g];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[4 * g + e] = v[e];
+    }
+#pragma unroll
+    for (int l = 1; l <= K; ++l)
+#pragma unroll
+        for (int t = 11; t >= 4 - K + l; --t) d[t] -= d[t - 1];
+    const bool edge = i0 < 8 || i0 + 8 > n;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t r = d[4 + k];
+        const uint32_t z = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+        zv[k] = (ResT)((!edge || (i0 + k >= K && i0 + k < n)) ? z : 0u);
+    }
+}
+
 /* floor(log2(x)) for a Rice mean x (normal, > 0): LDS thresholds, global table outside. */
 __device__ __forceinline__ int rice_floor_log2(double x, const double* tl, const double* gthr) {
     const int e = (int)((__double_as_longlong(x) >> 52) & 0x7ff) - 1023;
@@ -906,11 +933,22 @@ __device__ __forceinline__ void rice_params_wave0_multi(const ResidArgs& a, cons
     for (int j = 0; j < J; ++j) v[j] = fin[J * lane + j];
     int ekey = -1, esite = 0;
     uint32_t m5 = 0;
+    /* 32-bit residual rows: S < n * 2^32 <= 2^46 for n <= 16384, where the exact integer
+     * floor(log2(S / len)) equals the reference's float one (rice_params_wave0) */
+    const bool intlog = n <= 16384;
     auto param = [&](uint64_t S, int len, bool& zero, bool& neg) __attribute__((always_inline)) -> int {
         zero = S == 0;
         neg = false;
         if (zero) return 0;
-        const int prm = rice_floor_log2((double)S / (double)len, tl, a.log2thr);
+        int prm;
+        if (intlog) {
+            const int fs = 63 - __builtin_clzll((unsigned long long)S);
+            const int fl = 31 - __builtin_clz((unsigned)len);
+            prm = fs - fl;
+            if (prm >= 0 && ((uint64_t)len << prm) > S) --prm;
+        } else {
+            prm = rice_floor_log2((double)S / (double)len, tl, a.log2thr);
+        }
         neg = prm < 0;
         return prm;
     };
@@ -1795,10 +1833,16 @@ next_unit:
         }
     }
     wr_om = __builtin_amdgcn_readfirstlane(wr_om);
+    /* int8-MFMA units (|x| <= 2^23) that chose a fixed predictor: int32 difference chains */
+    const int wfk = __builtin_amdgcn_readfirstlane(
+        (MF8 && use_mf8 && dec->kind == FLACMI_KIND_FIXED && order <= 4) ? order : -1);
+    auto wide_pass = [&](auto kk) __attribute__((always_inline)) {
+    constexpr int KK = decltype(kk)::value;
 #pragma unroll 1
     for (int c = tid; c < nch; c += NT) {
         ResT zv[8];
-        resid_chunk(c, zv);
+        if constexpr (KK >= 0) fixed_resid_chunk32<KK>(xs32, 8 * c, n, zv);
+        else resid_chunk(c, zv);
         store_chunk(c, zv);
         if (WIDE && sizeof(ResT) == 4 && wr_om >= 0) {
             uint64_t cs8 = 0;
@@ -1814,6 +1858,19 @@ next_unit:
 #pragma unroll
             for (int k = 0; k < 8; ++k) zz[8 * c + k] = zv[k];
         }
+    }
+    };
+    if constexpr (MF8) {
+        switch (wfk) {
+            case 0: wide_pass(std::integral_constant<int, 0>{}); break;
+            case 1: wide_pass(std::integral_constant<int, 1>{}); break;
+            case 2: wide_pass(std::integral_constant<int, 2>{}); break;
+            case 3: wide_pass(std::integral_constant<int, 3>{}); break;
+            case 4: wide_pass(std::integral_constant<int, 4>{}); break;
+            default: wide_pass(std::integral_constant<int, -1>{}); break;
+        }
+    } else {
+        wide_pass(std::integral_constant<int, -1>{});
     }
     if (wide_flag) misc[2] = 1;
     __syncthreads();
@@ -1875,7 +1932,9 @@ next_unit:
              * (no heap pyramid, no barriers between orders, no contended atomics) */
             uint8_t* pk = reinterpret_cast<uint8_t*>(hs);
             if (wid == 0) {
-                if (P == 64) rice_params_wave0<false>(a, hs[P + lane], tl, rb, misc, pk, n, order, rmin, omax, lane);
+                if (P == 64 && n <= 16384) /* sums < 2^46: exact integer parameters */
+                    rice_params_wave0<true>(a, hs[P + lane], tl, rb, misc, pk, n, order, rmin, omax, lane);
+                else if (P == 64) rice_params_wave0<false>(a, hs[P + lane], tl, rb, misc, pk, n, order, rmin, omax, lane);
                 else if (P == 128) rice_params_wave0_multi<2>(a, hs + P, tl, rb, misc, pk, n, order, rmin, omax, lane);
                 else rice_params_wave0_multi<4>(a, hs + P, tl, rb, misc, pk, n, order, rmin, omax, lane);
             }
@@ -1969,32 +2028,37 @@ next_unit:
                     if (lane == 0) red[wid * 16 + o] = w;
                 }
             __syncthreads();
-            if (tid == 0) {
-                int best = -1;
-                unsigned long long bb = 0;
-                for (int o = rmin; o <= omax; ++o) {
-                    unsigned long long v = rb[o];
-                    for (int w2 = 0; w2 < nw; ++w2) v += red[w2 * 16 + o];
-                    if (best < 0 || v < bb) {
-                        bb = v;
-                        best = o;
-                    }
+            if (wid == 0) {
+                /* lane o: order o's total (its nw partials loaded side by side, not one thread
+                 * walking every order and wave); the first minimum (encoder.py:740-760) by
+                 * key = total * 16 + order over lanes 0..15 */
+                const bool cand = lane >= ro && lane <= oo;
+                unsigned long long v = 0;
+                if (cand) {
+                    v = rb[lane];
+                    for (int w2 = 0; w2 < nw; ++w2) v += red[w2 * 16 + lane];
                 }
-                put_meta(meta, ST_OK, 0, dec, 1);
-                meta->res_offset = start;
-                meta->res_len = n - start;
-                meta->part_order = best;
-                meta->n_parts = 1 << best;
-                meta->coding_method = ((misc[4] >> best) & 1) ? 5 : 4;
-                meta->rice_bits = (long long)bb;
-                misc[3] = best;
-            }
-            __syncthreads();
-            const int best = misc[3];
-            int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
-            for (int K = tid; K < (1 << best); K += NT) {
-                const int row = 16 * (K << (omax - best));
-                rp[K] = pk[row + 15] + pk[row + best]; /* pm + delta */
+                unsigned long long key = cand ? (v << 4) | (unsigned long long)lane : ~0ull;
+#pragma unroll
+                for (int s = 8; s >= 1; s >>= 1) {
+                    const unsigned long long t = __shfl_xor(key, s);
+                    key = t < key ? t : key;
+                }
+                const int best = __builtin_amdgcn_readfirstlane((int)(key & 15u));
+                if (lane == 0) {
+                    put_meta(meta, ST_OK, 0, dec, 1);
+                    meta->res_offset = start;
+                    meta->res_len = n - start;
+                    meta->part_order = best;
+                    meta->n_parts = 1 << best;
+                    meta->coding_method = ((misc[4] >> best) & 1) ? 5 : 4;
+                    meta->rice_bits = (long long)(key >> 4);
+                }
+                int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
+                for (int K = lane; K < (1 << best); K += 64) {
+                    const int row = 16 * (K << (omax - best));
+                    rp[K] = pk[row + 15] + pk[row + best]; /* pm + delta */
+                }
             }
             goto unit_done;
         }
