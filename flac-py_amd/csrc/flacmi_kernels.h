@@ -46,7 +46,9 @@ struct ResidArgs {
     int64_t* lpc_sums;       /* optional [count][32] */
     int32_t stop_after;      /* profiling ablation (env FLACMI_DEBUG_STOP): 0 = full kernel,
                                 1 = after staging, 2 = after candidate sums, 3 = after the
-                                choice, 4 = after the chosen residual; k_resid_stream prune
+                                choice, 4 = after the chosen residual (k_resid config-3
+                                Rice phase: 5 = after the parameters, 6 = after the row
+                                transform, 7 = after the data bits); k_resid_stream prune
                                 mode: 11 = bound tier 0 only, 12 = no LPC bound (wrong
                                 results, timing only) */
     int32_t mfma;            /* 1 = MFMA candidate sums where exact (env FLACMI_NO_MFMA=1 -> 0) */

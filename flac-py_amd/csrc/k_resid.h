@@ -914,112 +914,6 @@ __device__ __forceinline__ void rice_params_wave0(const ResidArgs& a, uint64_t s
     }
 }
 
-/* rice_params_wave0 for P = 64 J finest partitions (J = 2 or 4): lane k holds the sums of
- * finest partitions J k .. J k + J - 1 (fin = the heap's finest nodes, read before pk, which
- * aliases them, is written).  Orders omax .. omax - log2 J are lane-local (J >> d nodes per
- * lane), the coarser ones a butterfly over lanes as in rice_params_wave0.  Same outputs:
- * pk[16 f + o] for every finest partition f, rb[o] header bits, misc[0] the first error
- * (smallest order, then smallest partition: the reference's evaluation order), misc[1] its
- * site, misc[4] the orders with a parameter > 14.  Sums < 2^53: the parameter is the
- * reference's float floor(log2(S / len)) (rice_floor_log2). */
-template <int J>
-__device__ __forceinline__ void rice_params_wave0_multi(const ResidArgs& a, const unsigned long long* fin,
-                                                        const double* tl, unsigned long long* rb, int* misc,
-                                                        uint8_t* pk, int n, int order, int rmin, int omax,
-                                                        int lane) {
-    constexpr int LJ = J == 4 ? 2 : 1;
-    uint64_t v[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = fin[J * lane + j];
-    int ekey = -1, esite = 0;
-    uint32_t m5 = 0;
-    /* 32-bit residual rows: S < n * 2^32 <= 2^46 for n <= 16384, where the exact integer
-     * floor(log2(S / len)) equals the reference's float one (rice_params_wave0) */
-    const bool intlog = n <= 16384;
-    auto param = [&](uint64_t S, int len, bool& zero, bool& neg) __attribute__((always_inline)) -> int {
-        zero = S == 0;
-        neg = false;
-        if (zero) return 0;
-        int prm;
-        if (intlog) {
-            const int fs = 63 - __builtin_clzll((unsigned long long)S);
-            const int fl = 31 - __builtin_clz((unsigned)len);
-            prm = fs - fl;
-            if (prm >= 0 && ((uint64_t)len << prm) > S) --prm;
-        } else {
-            prm = rice_floor_log2((double)S / (double)len, tl, a.log2thr);
-        }
-        neg = prm < 0;
-        return prm;
-    };
-    /* lane-local orders: d = 0 .. LJ (J >> d nodes per lane, node K = (J >> d) lane + jj) */
-    static_for<LJ + 1>([&](auto D_) {
-        constexpr int d = D_;
-        constexpr int NJ = J >> d;
-        const int o = omax - d;
-        if (o >= rmin) {
-            if constexpr (d > 0) {
-#pragma unroll
-                for (int jj = 0; jj < NJ; ++jj) v[jj] = v[2 * jj] + v[2 * jj + 1];
-            }
-            uint32_t hb = 0;
-            int efirst = -1, ezero = 0;
-#pragma unroll
-            for (int jj = NJ - 1; jj >= 0; --jj) {
-                const int K = NJ * lane + jj;
-                const int len = (n >> o) - (K == 0 ? order : 0);
-                bool zero, neg;
-                const int prm = param(v[jj], len, zero, neg);
-#pragma unroll
-                for (int f = 0; f < (1 << d); ++f) pk[16 * (J * lane + (jj << d) + f) + o] = (uint8_t)prm;
-                if (zero || neg) efirst = jj, ezero = zero;
-                if (prm > 14) m5 |= 1u << o; /* made wave-uniform below */
-                hb += 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm);
-            }
-            const unsigned long long eb = __ballot(efirst >= 0);
-            if (eb) {
-                const int kl = __builtin_ctzll(eb);
-                ekey = (o << 16) | (NJ * kl + __shfl(efirst, kl));
-                esite = __shfl(ezero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
-            }
-            const uint32_t ht = wave_sum_u32(hb);
-            if (lane == 0) rb[o] = ht;
-        }
-    });
-    /* coarser orders: one node per 2^(d - LJ) lanes */
-    uint64_t t = v[0];
-    for (int o = omax - LJ - 1; o >= rmin; --o) {
-        const int d = omax - o - LJ; /* >= 1 */
-        t += (uint64_t)__shfl_xor((unsigned long long)t, 1 << (d - 1));
-        const int K = lane >> d;
-        const bool lead = (lane & ((1 << d) - 1)) == 0;
-        const int len = (n >> o) - (K == 0 ? order : 0);
-        bool zero, neg;
-        const int prm = param(t, len, zero, neg);
-#pragma unroll
-        for (int j = 0; j < J; ++j) pk[16 * (J * lane + j) + o] = (uint8_t)prm;
-        const unsigned long long eb = __ballot(lead && (zero || neg));
-        if (eb) {
-            const int kl = __builtin_ctzll(eb);
-            ekey = (o << 16) | (kl >> d);
-            esite = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
-        }
-        if (__ballot(lead && prm > 14)) m5 |= 1u << o;
-        const uint32_t hb = lead ? 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm) : 0u;
-        const uint32_t ht = wave_sum_u32(hb);
-        if (lane == 0) rb[o] = ht;
-    }
-    /* lane-local m5 bits: OR over the wave */
-    uint32_t mo = m5;
-#pragma unroll
-    for (int sft = 32; sft >= 1; sft >>= 1) mo |= (uint32_t)__shfl_xor((int)mo, sft);
-    if (lane == 0) {
-        misc[0] = ekey;
-        misc[1] = esite;
-        misc[4] = (int)mo;
-    }
-}
-
 /* data bits of one chunk for every candidate order (chunk sum < 2^30 for narrow values) */
 __device__ __forceinline__ void chunk_rice_bits(const uint32_t (&z)[8], uint4 pv, int ro, int oo,
                                                 uint32_t (&tb)[16]) {
@@ -1251,6 +1145,17 @@ next_unit:
     /* the unit's LPC status: loaded now, tested after the staging loads are in flight (a
      * test here would put one more HBM round trip in front of them) */
     const int st_rec = ref_mode ? rec[0] : 0;
+    /* int8-MFMA builds: the record's words tid and tid + NT, loaded beside the samples (the
+     * coefficient table is scattered from them after the staging loop instead of gathered
+     * from HBM in a second round trip); clamped indices, no guarded loads */
+    int32_t rv[2] = {0, 0};
+    const bool rec_regs = MF8 && do_lpc && 2 * NT >= a.rec_words;
+    if constexpr (MF8) {
+        if (rec_regs) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) rv[j] = rec[min(tid + j * NT, a.rec_words - 1)];
+        }
+    }
     if constexpr (S16) {
         for (int i = tid; i < HP; i += NT) xs16[i - HP] = 0;
         for (int i = n + tid; i < resid_xpad(n); i += NT) xs16[i] = 0;
@@ -1361,9 +1266,28 @@ next_unit:
     }
     if (do_lpc) {
         const uint32_t negmask = (uint32_t)rec[1];
-        for (int i = tid; i < LMAX * CT::CPAD; i += NT) {
-            const int pp = i / CT::CPAD + 1, j = i % CT::CPAD;
-            cfl[i] = (pp <= L && j < pp) ? rec[2 + L + (pp * (pp - 1)) / 2 + j] : 0;
+        if (MF8 && rec_regs) {
+            /* the table's zeros, then every coefficient word w = 2 + L + pp (pp - 1) / 2 + j
+             * from the thread that holds it (disjoint entries: no barrier between) */
+            for (int i = tid; i < LMAX * CT::CPAD; i += NT) {
+                const int pp = i / CT::CPAD + 1, j = i % CT::CPAD;
+                if (!(pp <= L && j < pp)) cfl[i] = 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int w = tid + k * NT - 2 - L;
+                if (w >= 0 && w < (L * (L + 1)) / 2) {
+                    int pp = (int)((1.0f + __builtin_sqrtf(1.0f + 8.0f * (float)w)) * 0.5f);
+                    if ((pp * (pp - 1)) / 2 > w) --pp;
+                    if ((pp * (pp + 1)) / 2 <= w) ++pp;
+                    cfl[(pp - 1) * CT::CPAD + (w - (pp * (pp - 1)) / 2)] = rv[k];
+                }
+            }
+        } else {
+            for (int i = tid; i < LMAX * CT::CPAD; i += NT) {
+                const int pp = i / CT::CPAD + 1, j = i % CT::CPAD;
+                cfl[i] = (pp <= L && j < pp) ? rec[2 + L + (pp * (pp - 1)) / 2 + j] : 0;
+            }
         }
         /* pair t of order pp: (lo = c[2t], hi = c[2t-1]) with c[-1] = -2^shift (S16 and
          * W64S paths only) */
@@ -1823,7 +1747,7 @@ next_unit:
     if constexpr (!FAST) {
     /* WIDE, 32-bit rows, 64..256 finest partitions of at most 64 whole chunks each: the
      * finest partition sums are reduced here across the cpp consecutive lanes that own a
-     * partition's chunks, into the heap's finest nodes, for rice_params_wave0(_multi) */
+     * partition's chunks, into the heap's finest nodes, for the per-node parameter step */
     int wr_om = -1, wr_cpp = 0;
     if constexpr (WIDE && sizeof(ResT) == 4) {
         const int om = first_order();
@@ -1928,47 +1852,116 @@ next_unit:
     }
     if constexpr (WIDE && sizeof(ResT) == 4) {
         if (wr_om >= 0) {
-            /* wave 0: every order's parameters from the finest sums phase E left in hs[P..2P)
-             * (no heap pyramid, no barriers between orders, no contended atomics) */
+            /* Every heap node's parameter at once (encoder.py:655-760), one node per thread:
+             *  1. wave 0: prefix sums of the finest sums (hs[P..2P), left by phase E) into the
+             *     generic path's heap-parameter region (unused here): pre(k), k = 1..P;
+             *  2. node j = 2^o + K (orders rmin..omax): S = pre[(K+1) 2^d] - pre[K 2^d], d =
+             *     omax - o, its parameter into prmN[j], header bits summed per order (wave sums,
+             *     one LDS atomic per wave and order), the first error in the reference's
+             *     evaluation order (orders, then partitions: the smallest j) by atomicMin;
+             *  3. finest partition k: its ancestors' parameters gathered into its 16-byte row
+             *     (byte o = p_o - pm, byte 14 = some delta >= 16, byte 15 = pm), where pk aliases
+             *     the finest sums step 1 has consumed.
+             * No node waits on another order, and no wave runs the parameters alone. */
             uint8_t* pk = reinterpret_cast<uint8_t*>(hs);
+            /* pre(k) = sum of the finest sums below k: preA[k - 1] (8P bytes, the size of hp);
+             * node parameters in the coefficient region (>= 1280 bytes, dead since phase E) */
+            unsigned long long* preA = reinterpret_cast<unsigned long long*>(hp); /* [P] */
+            uint8_t* prmN = reinterpret_cast<uint8_t*>(smem + lay.coef);        /* [2P] */
+            const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
             if (wid == 0) {
-                if (P == 64 && n <= 16384) /* sums < 2^46: exact integer parameters */
-                    rice_params_wave0<true>(a, hs[P + lane], tl, rb, misc, pk, n, order, rmin, omax, lane);
-                else if (P == 64) rice_params_wave0<false>(a, hs[P + lane], tl, rb, misc, pk, n, order, rmin, omax, lane);
-                else if (P == 128) rice_params_wave0_multi<2>(a, hs + P, tl, rb, misc, pk, n, order, rmin, omax, lane);
-                else rice_params_wave0_multi<4>(a, hs + P, tl, rb, misc, pk, n, order, rmin, omax, lane);
+                const int J = P >> 6; /* finest partitions per lane: 1, 2 or 4 */
+                uint64_t v[4] = {0, 0, 0, 0}, t = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (j < J) v[j] = hs[P + J * lane + j], t += v[j];
+                uint64_t inc = t; /* inclusive scan of the lane totals */
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint64_t u = (uint64_t)__shfl_up((unsigned long long)inc, (unsigned)d);
+                    if (lane >= d) inc += u;
+                }
+                uint64_t e = inc - t;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (j < J) e += v[j], preA[J * lane + j] = e;
+                if (lane < 16) rb[lane] = 0;
+                if (lane == 0) misc[0] = 0x7fffffff, misc[4] = 0;
             }
             __syncthreads();
-            if (misc[0] >= 0) {
-                if (tid == 0) put_meta(meta, ST_VALUE, misc[1], dec, 1);
+            {
+                const bool intlog = n <= 16384; /* S < n 2^32 <= 2^46: exact integer floor(log2(S / len)) */
+                for (int j0 = (1 << ro); j0 < 2 * P; j0 += NT) {
+                    const int j = j0 + tid;
+                    const bool live = j < 2 * P;
+                    const int o = live ? 31 - __builtin_clz((unsigned)j) : 0;
+                    uint32_t hb = 0;
+                    bool big = false;
+                    if (live) {
+                        const int K = j - (1 << o), d = omax - o;
+                        const uint64_t S = preA[((K + 1) << d) - 1] - (K > 0 ? preA[(K << d) - 1] : 0ull);
+                        const int len = (n >> o) - (K == 0 ? order : 0);
+                        int prm = 0;
+                        if (S != 0) {
+                            if (intlog) {
+                                const int fs = 63 - __builtin_clzll((unsigned long long)S);
+                                const int fl = 31 - __builtin_clz((unsigned)len);
+                                prm = fs - fl;
+                                if (prm >= 0 && ((uint64_t)len << prm) > S) --prm;
+                            } else {
+                                prm = rice_floor_log2((double)S / (double)len, tl, a.log2thr);
+                            }
+                        }
+                        prmN[j] = (uint8_t)prm;
+                        if (S == 0 || prm < 0) atomicMin(&misc[0], (j << 1) | (S == 0 ? 1 : 0));
+                        big = prm > 14;
+                        hb = 4u + (prm > 14 ? 5u : 4u) + (uint32_t)len * (uint32_t)(1 + prm);
+                    }
+                    /* header bits: one wave sum per order this wave's nodes span; the orders with a
+                     * parameter > 14 (five-bit coding) by ballot, one LDS atomic per wave */
+                    const int jw = __builtin_amdgcn_readfirstlane(j);
+                    const int ow0 = 31 - __builtin_clz((unsigned)jw);
+                    const int jl = min(jw + 63, 2 * P - 1);
+                    const int ow1 = 31 - __builtin_clz((unsigned)jl);
+                    for (int ow = ow0; ow <= ow1; ++ow) {
+                        const uint32_t hs32 = wave_sum_u32(live && o == ow ? hb : 0u);
+                        if (lane == 0 && jw < 2 * P) atomicAdd(&rb[ow], (unsigned long long)hs32);
+                        if (__ballot(live && o == ow && big) && lane == 0) atomicOr(&misc[4], 1 << ow);
+                    }
+                }
+            }
+            __syncthreads();
+            if (a.stop_after == 5) goto unit_done; /* ablation: after the parameters */
+            if (misc[0] != 0x7fffffff) {
+                if (tid == 0)
+                    put_meta(meta, ST_VALUE, (misc[0] & 1) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT,
+                             dec, 1);
                 goto unit_done;
             }
             const int cpp = ps >> 3;
-            const int ro = __builtin_amdgcn_readfirstlane(rmin), oo = __builtin_amdgcn_readfirstlane(omax);
-            /* each finest partition's row: byte o = p_o - pm for the candidate orders, byte 15 =
-             * pm = their smallest parameter (orders <= 12, so byte 15 is free).  Then
-             * sum(z >> p_o) = sum(y >> (p_o - pm)) with y = z >> pm, and y mostly fits 16 bits:
-             * two values per v_pk_lshrrev_b16 + v_dot2_u32_u16 */
             for (int k = tid; k < P; k += NT) {
-                uint32_t* r = reinterpret_cast<uint32_t*>(pk + 16 * k);
-                uint32_t w[4] = {r[0], r[1], r[2], r[3]};
-                uint32_t pm = 255;
+                uint32_t w[4] = {0, 0, 0, 0};
+                uint32_t pm = 255, dmax = 0;
+                uint32_t pv[13];
+#pragma unroll
+                for (int o = 0; o < 13; ++o) {
+                    pv[o] = (o >= ro && o <= oo) ? prmN[(1 << o) + (k >> (omax - o))] : 0u;
+                    if (o >= ro && o <= oo) pm = min(pm, pv[o]);
+                }
 #pragma unroll
                 for (int o = 0; o < 13; ++o)
-                    if (o >= ro && o <= oo) pm = min(pm, (w[o >> 2] >> (8 * (o & 3))) & 0xffu);
-#pragma unroll
-                for (int o = 0; o < 13; ++o)
-                    if (o >= ro && o <= oo) w[o >> 2] -= pm << (8 * (o & 3));
+                    if (o >= ro && o <= oo) {
+                        const uint32_t dl = pv[o] - pm;
+                        dmax = max(dmax, dl);
+                        w[o >> 2] |= dl << (8 * (o & 3));
+                    }
                 /* byte 14: some delta >= 16 (v_pk_lshrrev_b16 shifts by the amount mod 16, so such
                  * a row takes the 32-bit path) */
-                uint32_t dmax = 0;
-#pragma unroll
-                for (int o = 0; o < 13; ++o)
-                    if (o >= ro && o <= oo) dmax = max(dmax, (w[o >> 2] >> (8 * (o & 3))) & 0xffu);
-                w[3] = (w[3] & 0x0000ffffu) | ((dmax >= 16 ? 1u : 0u) << 16) | (pm << 24);
-                r[0] = w[0], r[1] = w[1], r[2] = w[2], r[3] = w[3];
+                w[3] |= ((dmax >= 16 ? 1u : 0u) << 16) | (pm << 24);
+                *reinterpret_cast<uint4*>(pk + 16 * k) = uint4{w[0], w[1], w[2], w[3]};
             }
             __syncthreads();
+            if (a.stop_after == 6) goto unit_done; /* ablation: after the row transform */
             const uint4* pkv = reinterpret_cast<const uint4*>(hs);
             uint64_t tb[16];
             uint32_t tp[16]; /* packed-path totals: this thread's sum(y >> d) < 4 * 8 * 2^16 per order */
@@ -2021,6 +2014,10 @@ next_unit:
             }
 #pragma unroll
             for (int o = 0; o < 16; ++o) tb[o] += tp[o];
+            if (a.stop_after == 7) { /* ablation: after the data bits (kept live) */
+                if (tb[0] == 0x9e3779b9u) meta->reserved0 = 1;
+                goto unit_done;
+            }
 #pragma unroll
             for (int o = 0; o < 16; ++o)
                 if (o >= ro && o <= oo) {
