@@ -155,6 +155,26 @@ __device__ __forceinline__ void put_meta(flacmi_unit_meta* m, int status, int si
     for (int j = 0; j < FLACMI_MAX_LPC_ORDER; ++j) m->coefs[j] = (with_choice && j < d->ncoefs) ? d->coef[j] : 0;
 }
 
+/* put_meta(.., with_choice = 1) plus the Rice fields, by one wave: lane i writes dword i of
+ * the 52-dword record (one coalesced store instead of ~50 single-lane stores, each behind
+ * its own LDS read of the decision) */
+__device__ __forceinline__ void put_meta_wave(flacmi_unit_meta* m, int lane, int status, int site, const Decision* d,
+                                              int res_offset, int res_len, int part_order, int n_parts, int coding,
+                                              long long rice_bits) {
+    const int j = lane - 20;
+    uint32_t x = (j >= 0 && j < d->ncoefs) ? (uint32_t)d->coef[j < FLACMI_MAX_LPC_ORDER ? j : 0] : 0u;
+    const uint32_t f[20] = {(uint32_t)status, (uint32_t)site, (uint32_t)d->kind, (uint32_t)d->order,
+                            (uint32_t)d->shift, (uint32_t)d->ncoefs, (uint32_t)res_offset, (uint32_t)res_len,
+                            (uint32_t)d->fixed_order, (uint32_t)d->lpc_order, (uint32_t)part_order,
+                            (uint32_t)n_parts, (uint32_t)coding, 0u, (uint32_t)d->fixed_sum,
+                            (uint32_t)((unsigned long long)d->fixed_sum >> 32), (uint32_t)d->lpc_sum,
+                            (uint32_t)((unsigned long long)d->lpc_sum >> 32), (uint32_t)rice_bits,
+                            (uint32_t)((unsigned long long)rice_bits >> 32)};
+#pragma unroll
+    for (int i = 0; i < 20; ++i) x = lane == i ? f[i] : x;
+    if (lane < 52) reinterpret_cast<uint32_t*>(m)[lane] = x;
+}
+
 /* Workgroup size of k_resid for n samples: 8-sample chunks, up to kCPT per thread while
  * the workgroup stays <= 256 threads (512 for the 64-bit paths: their long blocks fill the
  * LDS with one workgroup per CU, so 8 waves are two per SIMD), more beyond that.  The

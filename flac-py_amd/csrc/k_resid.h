@@ -1751,7 +1751,11 @@ next_unit:
     int wr_om = -1, wr_cpp = 0;
     if constexpr (WIDE && sizeof(ResT) == 4) {
         const int om = first_order();
-        if (om >= 6 && om <= 8 && ((n >> om) & 7) == 0 && (n >> om) >> 3 <= 64 && a.mode != FLACMI_MODE_LPC_ONLY) {
+        const int cpp = (n >> om) >> 3;
+        /* the chunk sums reduce over a partition's lanes by a butterfly: cpp a power of two
+         * (n = 4608 at order 6 has 9 chunks per partition: the generic heap path takes it) */
+        if (om >= 6 && om <= 8 && ((n >> om) & 7) == 0 && cpp <= 64 && (cpp & (cpp - 1)) == 0 &&
+            a.mode != FLACMI_MODE_LPC_ONLY) {
             wr_om = om;
             wr_cpp = (n >> om) >> 3;
         }
@@ -2018,12 +2022,27 @@ next_unit:
                 if (tb[0] == 0x9e3779b9u) meta->reserved0 = 1;
                 goto unit_done;
             }
+            {
+                uint64_t any = 0;
 #pragma unroll
-            for (int o = 0; o < 16; ++o)
-                if (o >= ro && o <= oo) {
-                    const uint64_t w = wave_sum_u64(tb[o]);
-                    if (lane == 0) red[wid * 16 + o] = w;
+                for (int o = 0; o < 16; ++o) any |= (o >= ro && o <= oo) ? tb[o] : 0ull;
+                /* every lane < 2^26: 32-bit wave sums (a wave-uniform branch) */
+                if (__ballot(any >= (1ull << 26)) == 0) {
+#pragma unroll
+                    for (int o = 0; o < 16; ++o)
+                        if (o >= ro && o <= oo) {
+                            const uint32_t w = wave_sum_u32((uint32_t)tb[o]);
+                            if (lane == 0) red[wid * 16 + o] = w;
+                        }
+                } else {
+#pragma unroll
+                    for (int o = 0; o < 16; ++o)
+                        if (o >= ro && o <= oo) {
+                            const uint64_t w = wave_sum_u64(tb[o]);
+                            if (lane == 0) red[wid * 16 + o] = w;
+                        }
                 }
+            }
             __syncthreads();
             if (wid == 0) {
                 /* lane o: order o's total (its nw partials loaded side by side, not one thread
@@ -2042,15 +2061,11 @@ next_unit:
                     key = t < key ? t : key;
                 }
                 const int best = __builtin_amdgcn_readfirstlane((int)(key & 15u));
-                if (lane == 0) {
-                    put_meta(meta, ST_OK, 0, dec, 1);
-                    meta->res_offset = start;
-                    meta->res_len = n - start;
-                    meta->part_order = best;
-                    meta->n_parts = 1 << best;
-                    meta->coding_method = ((misc[4] >> best) & 1) ? 5 : 4;
-                    meta->rice_bits = (long long)(key >> 4);
-                }
+                const unsigned long long bits = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane(
+                                                     (int)(uint32_t)(key >> 36)) << 32) |
+                                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(key >> 4));
+                put_meta_wave(meta, lane, ST_OK, 0, dec, start, n - start, best, 1 << best,
+                              ((misc[4] >> best) & 1) ? 5 : 4, (long long)bits);
                 int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
                 for (int K = lane; K < (1 << best); K += 64) {
                     const int row = 16 * (K << (omax - best));

@@ -377,10 +377,11 @@ def test_wide_chosen_residual_redoes_only_those_units(az):
     compare_with_oracle(out, ora, [n] * (nu - 1) + [700])
 
 
-@pytest.mark.parametrize("n,rmax", [(4096, 8), (2048, 6), (8192, 7)])
+@pytest.mark.parametrize("n,rmax", [(4096, 8), (2048, 6), (8192, 7), (4608, 6), (12288, 7), (6144, 8)])
 def test_wide_rice_wave0_parameters_and_errors(az, n, rmax):
-    """PATH_W64 with 64..256 finest partitions: wave 0 derives every order's parameters from
-    the finest sums phase E reduced (rice_params_wave0 / _multi).  Silent stretches give a zero
+    """PATH_W64 with 64..256 finest partitions: the heap nodes' parameters come from the
+    finest sums phase E reduced across the lanes that own a partition's chunks (4608/6,
+    12288/7, 6144/8: 9, 12 and 3 chunks per finest partition, not a power of two).  Silent stretches give a zero
     partition sum (log of 0: ValueError), sparse +-1 stretches a mean below 1 (negative
     parameter); loud units exercise Rice5Bit parameters (> 14) at every level."""
     r = np.random.default_rng(n + rmax)
