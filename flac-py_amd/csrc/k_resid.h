@@ -596,8 +596,13 @@ __device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const un
 #pragma unroll
                 for (int e = 0; e < 4; ++e) x12[4 * g + e] = v[e];
             }
-            if (i0 >= 8) fixed_sums32<false>(x12, i0, n, fa);
-            else fixed_sums32<true>(x12, i0, n, fa);
+            /* a chunk's sums in 32 bits (|x| <= 2^23 on this path: 8 |D4| < 2^30), so each |D|
+             * is one v_sad_u32 into its accumulator; 64 bits once per chunk and order */
+            uint32_t ca[5] = {0, 0, 0, 0, 0};
+            if (i0 >= 8) fixed_sums32<false>(x12, i0, n, ca);
+            else fixed_sums32<true>(x12, i0, n, ca);
+#pragma unroll
+            for (int o = 0; o < 5; ++o) fa[o] += ca[o];
         }
 #pragma unroll
         for (int o = 0; o < 5; ++o) {
