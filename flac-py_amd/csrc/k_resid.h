@@ -773,6 +773,7 @@ __device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const un
     for (int t = 0; t < kTiers; ++t) {
         const int res = (int)((0x73516240u >> (4 * t)) & 15u);
         go(wid + res * nw, kTiers * nw);
+        if (t == 0) continue; /* the first test after two eighths (few units stop after one) */
         store();
         if (t == kTiers - 1) break; /* every tile done: the sums are exact */
         __syncthreads();
