@@ -568,7 +568,7 @@ __device__ __forceinline__ void mf8_tile_epilogue(const v4i (&D)[4], int s, cons
  * cfl / lsh: phase A's coefficient and shift tables; G: tiles per u32 partial sum.
  *
  * prune (reference mode): the tiles run in eight tiers, the wave's tiles k % 8 == 0, then
- * 4, 2, 6, 1, 5, 3, 7.  After each tier every wave reads the workgroup's exact partial LPC sums (a sum
+ * 4, 2, 6, 1, 5, 3, 7.  After each tier from the second on, every wave reads the workgroup's exact partial LPC sums (a sum
  * over a subset of the values, so a lower bound of each order's full sum) against the best
  * exact fixed sum; once every order's partial sum exceeds it, LPC can neither win nor tie
  * (encoder.py:135-157) and the remaining tiers are skipped: returns true (workgroup-uniform;
