@@ -772,8 +772,13 @@ __device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const un
 #pragma unroll 1
     for (int t = 0; t < kTiers; ++t) {
         const int res = (int)((0x73516240u >> (4 * t)) & 15u);
-        go(wid + res * nw, kTiers * nw);
-        if (t == 0) continue; /* the first test after two eighths (few units stop after one) */
+        if (t == 0) { /* the first test after two eighths (few units stop after one): residues 0
+                       * and 4 as one quarter, one pipelined run */
+            go(wid, 4 * nw);
+            ++t;
+        } else {
+            go(wid + res * nw, kTiers * nw);
+        }
         store();
         if (t == kTiers - 1) break; /* every tile done: the sums are exact */
         __syncthreads();
@@ -1780,8 +1785,15 @@ next_unit:
         store_chunk(c, zv);
         if (WIDE && sizeof(ResT) == 4 && wr_om >= 0) {
             uint64_t cs8 = 0;
+            if constexpr (KK >= 0) { /* difference chains: every value < 2^28, eight < 2^31 */
+                uint32_t c32 = 0;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cs8 += (uint64_t)zv[k];
+                for (int k = 0; k < 8; ++k) c32 += (uint32_t)zv[k];
+                cs8 = c32;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) cs8 += (uint64_t)zv[k];
+            }
             for (int w = 1; w < wr_cpp; w <<= 1) cs8 += (uint64_t)__shfl_xor((unsigned long long)cs8, w);
             if ((c & (wr_cpp - 1)) == 0) hs[(1 << wr_om) + c / wr_cpp] = cs8;
         }
