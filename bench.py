@@ -338,12 +338,38 @@ def shard_first_unit(rank, units_per_rank):
     return rank * units_per_rank
 
 
-def reduce_stats(stats, dist=None):
-    """Stream totals over ranks: the one collective of the multi-GPU path (RCCL over xGMI
-    on the GPU; the gloo CPU tests exercise the same call)."""
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+def reduce_stats(stats, dist=None, comm=None, stream=0):
+    """Stream totals over ranks: the one collective of the multi-GPU path.  On the GPU it is
+    the C-ABI's flacmi_allreduce_stats (RCCL over xGMI, `comm` a flac_amd StatsComm, on the
+    launch stream); without a comm (the gloo CPU tests) the same sum over torch.distributed."""
+    if comm is not None:
+        comm.allreduce_stats(stats.data_ptr(), stream)
+    elif dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(stats)
     return stats
+
+
+def broadcast_comm_id(cid, dist, nbytes, device=None):
+    """Rank 0's flacmi_comm_id bytes (ncclUniqueId) to every rank over the existing process
+    group, so each rank can build the C-ABI communicator (flacmi_comm_init)."""
+    import torch
+    t = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+    if dist.get_rank() == 0:
+        if cid is None or len(cid) != nbytes:
+            raise ValueError(f"rank 0 needs a {nbytes}-byte comm id")
+        t.copy_(torch.frombuffer(bytearray(cid), dtype=torch.uint8))
+    dist.broadcast(t, 0)
+    return bytes(t.cpu().numpy().tobytes())
+
+
+def open_stats_comm(az, dist, rank, world, device):
+    """The C-ABI stats communicator of an N-rank job: rank 0's id broadcast over the process
+    group, then flacmi_comm_init on every rank (a collective call)."""
+    from flac_amd import abi
+    from flac_amd.analysis import StatsComm
+    cid = StatsComm.comm_id(az.lib) if rank == 0 else None
+    cid = broadcast_comm_id(cid, dist, abi.COMM_ID_BYTES, device)
+    return StatsComm(az, world, rank, cid)
 
 
 def reduce_elapsed(elapsed, dist=None, device=None):
@@ -412,10 +438,19 @@ def launch_check(args, cfg, units):
     st = torch.tensor([mine, mine * cfg["n"], lo, hi, 1 << rank], dtype=torch.int64)
     reduce_stats(st, dist)
     el = reduce_elapsed(0.001 * (rank + 1), dist)
+    id_ok = None
+    if world > 1:
+        # the comm-id hand-off the GPU path makes before flacmi_comm_init (a fixed 128-byte
+        # pattern stands in for rank 0's ncclUniqueId); every rank must hold rank 0's bytes
+        pattern = bytes((i * 37 + 11) % 256 for i in range(128))
+        got = broadcast_comm_id(pattern if rank == 0 else None, dist, 128)
+        ok = torch.tensor([int(got == pattern)], dtype=torch.int64)
+        dist.all_reduce(ok)
+        id_ok = int(ok.item()) == world
     if rank == 0:
         print(json.dumps({"launch_check": True, "world_size": world, "gpus_arg": args.gpus, "config": args.config,
                           "units_total": int(st[0]), "samples_total": int(st[1]), "expected_units": total,
-                          "rank_mask": int(st[4]), "elapsed_max": el}), flush=True)
+                          "rank_mask": int(st[4]), "elapsed_max": el, "comm_id_broadcast_ok": id_ok}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -473,20 +508,35 @@ def main(argv=None):
 
     stats_acc = torch.zeros_like(stats)
     bufs = dict(samples=samples, meta=meta, rparams=rparams, residual=residual, stats=stats, stats_acc=stats_acc)
+    # N > 1: the stream totals go through the C-ABI collective (flacmi_allreduce_stats)
+    comm = open_stats_comm(az, dist, rank, world, dev) if distributed else None
 
     def step():
         if not chunked:
             az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, units, n, params, meta.data_ptr(),
                               rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, sptr)
             az.stream_stats(meta.data_ptr(), units, n, stats.data_ptr(), sptr)
-            reduce_stats(stats, dist)
+            reduce_stats(stats, dist, comm, sptr)
             return
         run_chunks(az, cfg, params, bufs, my_chunks, units, total_units, args.seed, sptr)
-        reduce_stats(stats_acc, dist)
+        reduce_stats(stats_acc, dist, comm, sptr)
         stats.copy_(stats_acc)
 
     for _ in range(args.warmup):
         step()
+    if comm is not None:
+        # the C-ABI reduce must equal torch.distributed's sum of the same per-rank vectors
+        # (outside the timed region: one more step's local stats, reduced both ways)
+        local_stats = (stats_acc if chunked else stats).clone()
+        if not chunked:
+            az.stream_stats(meta.data_ptr(), units, n, local_stats.data_ptr(), sptr)
+        via_torch = local_stats.clone()
+        torch.cuda.synchronize(dev)
+        dist.all_reduce(via_torch)
+        reduce_stats(local_stats, dist, comm, sptr)
+        torch.cuda.synchronize(dev)
+        if not torch.equal(local_stats, via_torch):
+            raise SystemExit(f"rank {rank}: flacmi_allreduce_stats differs from torch.distributed's all_reduce")
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -577,7 +627,8 @@ def main(argv=None):
             "config": {"workload": cfg["workload"], "units_per_gpu": total_units // world,
                        "units_total": total_units, "chunk_units": units if chunked else None, "block": n, "sample_bits": bits,
                        "max_lpc_order": cfg["L"], "qlp_precision": cfg["q"], "rice": [cfg["rmin"], cfg["rmax"]],
-                       "mode": "fixed-only" if cfg["mode"] else "reference", "parallelism": f"dp{world} (block shards)"},
+                       "mode": "fixed-only" if cfg["mode"] else "reference", "parallelism": f"dp{world} (block shards)",
+                       "stats_collective": "flacmi_allreduce_stats (C-ABI, RCCL)" if comm is not None else None},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": dom_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dom_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": (os.path.relpath(tfile, REPO) + ": rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
@@ -599,6 +650,8 @@ def main(argv=None):
                              "errors": int(st[65:80].sum())},
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     az.close()
     if distributed:
         dist.destroy_process_group()

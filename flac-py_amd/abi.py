@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2  # include/flacmi.h FLACMI_ABI_VERSION
 MAX_LPC_ORDER = 32
 MAX_BLOCK = 65535
 MAX_RICE_ORDER = 15
@@ -61,6 +61,8 @@ SITE_NAMES = {
     17: "frame of 2^28 bytes or more (not packed by this build)",
 }
 
+SITE_CHOICE_TIE = 10  # FLACMI_SITE_CHOICE_TIE
+
 MODE_REFERENCE = 0
 MODE_FIXED_ONLY = 1
 MODE_LPC_ONLY = 2
@@ -110,7 +112,7 @@ class UnitMeta(C.Structure):
         ("part_order", C.c_int32),
         ("n_parts", C.c_int32),
         ("coding_method", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("lpc_tiers", C.c_int32),
         ("fixed_sum", C.c_int64),
         ("lpc_sum", C.c_int64),
         ("rice_bits", C.c_int64),
@@ -123,7 +125,7 @@ META_DTYPE = np.dtype([
     ("status", "<i4"), ("site", "<i4"), ("kind", "<i4"), ("order", "<i4"),
     ("shift", "<i4"), ("ncoefs", "<i4"), ("res_offset", "<i4"), ("res_len", "<i4"),
     ("fixed_order", "<i4"), ("lpc_order", "<i4"), ("part_order", "<i4"), ("n_parts", "<i4"),
-    ("coding_method", "<i4"), ("reserved0", "<i4"),
+    ("coding_method", "<i4"), ("lpc_tiers", "<i4"),
     ("fixed_sum", "<i8"), ("lpc_sum", "<i8"), ("rice_bits", "<i8"),
     ("coefs", "<i4", (MAX_LPC_ORDER,)),
 ])

@@ -126,6 +126,7 @@ __device__ __forceinline__ uint64_t uabs64(int64_t v) { return v < 0 ? (uint64_t
 
 struct Decision {
     int status, site, kind, order, shift, ncoefs, fixed_order, lpc_order;
+    int tiers; /* meta.lpc_tiers: LPC candidate passes made | passes of the path << 8 (0: no pruning) */
     long long fixed_sum, lpc_sum;
     int coef[FLACMI_MAX_LPC_ORDER];
 };
@@ -148,7 +149,7 @@ __device__ __forceinline__ void put_meta(flacmi_unit_meta* m, int status, int si
     m->part_order = 0;
     m->n_parts = 0;
     m->coding_method = 0;
-    m->reserved0 = 0;
+    m->lpc_tiers = d ? d->tiers : 0;
     m->fixed_sum = d ? d->fixed_sum : 0;
     m->lpc_sum = d ? d->lpc_sum : 0;
     m->rice_bits = 0;
@@ -166,7 +167,7 @@ __device__ __forceinline__ void put_meta_wave(flacmi_unit_meta* m, int lane, int
     const uint32_t f[20] = {(uint32_t)status, (uint32_t)site, (uint32_t)d->kind, (uint32_t)d->order,
                             (uint32_t)d->shift, (uint32_t)d->ncoefs, (uint32_t)res_offset, (uint32_t)res_len,
                             (uint32_t)d->fixed_order, (uint32_t)d->lpc_order, (uint32_t)part_order,
-                            (uint32_t)n_parts, (uint32_t)coding, 0u, (uint32_t)d->fixed_sum,
+                            (uint32_t)n_parts, (uint32_t)coding, (uint32_t)d->tiers, (uint32_t)d->fixed_sum,
                             (uint32_t)((unsigned long long)d->fixed_sum >> 32), (uint32_t)d->lpc_sum,
                             (uint32_t)((unsigned long long)d->lpc_sum >> 32), (uint32_t)rice_bits,
                             (uint32_t)((unsigned long long)rice_bits >> 32)};

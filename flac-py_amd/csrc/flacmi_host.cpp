@@ -929,12 +929,18 @@ static void enc_free(EncState* es) {
 
 static int enc_state(flacmi_ctx* ctx, int64_t per_nf, EncState** out) {
     if (!ctx->enc) {
+        /* built whole before it is published: a failed create leaves no half state behind */
         EncState* es = new EncState();
-        ctx->enc = es;
-        HIP_TRY(hipStreamCreateWithFlags(&es->is, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&es->os, hipStreamNonBlocking));
+        hipError_t e = hipStreamCreateWithFlags(&es->is, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&es->os, hipStreamNonBlocking);
         for (auto& sl : es->slot)
-            for (auto& e : sl.e) HIP_TRY(hipEventCreate(&e));
+            for (auto& ev : sl.e)
+                if (e == hipSuccess) e = hipEventCreate(&ev);
+        if (e != hipSuccess) {
+            enc_free(es);
+            return fail(FLACMI_E_HIP, "encode pipeline state: %s", hipGetErrorString(e));
+        }
+        ctx->enc = es;
     }
     EncState* es = ctx->enc;
     if (es->cap_nf < per_nf) {
@@ -961,9 +967,11 @@ static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, co
                      const flacmi_frame_params* fp, hipStream_t cs, hipStream_t is) {
     const flacmi_batch& b = sl.b;
     const size_t nu = (size_t)b.n_units;
-    /* rows whose stride is a multiple of 16 bytes keep it on the device: one linear copy */
-    const bool linear = (whole->unit_stride * b.sample_bytes) % 16 == 0;
-    sl.dstride = linear ? whole->unit_stride : ((b.block_len * b.sample_bytes + 15) / 16) * 16 / b.sample_bytes;
+    /* rows already at the padded device stride go as one linear copy; any other stride (a
+       row view of a wider array) is packed to padded device rows by a 2-D copy */
+    const int64_t padded = ((b.block_len * b.sample_bytes + 15) / 16) * 16 / b.sample_bytes;
+    const bool linear = whole->unit_stride == padded;
+    sl.dstride = padded;
     const int64_t sstride = sl.dstride;
     const int64_t pstride = (1LL << (params->rice_max > 0 ? params->rice_max : 0)) + 1;
     const int64_t rstride = ((b.block_len * sl.rbytes + 15) / 16) * 16 / sl.rbytes;
@@ -1304,6 +1312,7 @@ int flacmi_comm_destroy(flacmi_comm* comm) {
     if (!comm) return 0;
     int rc = 0;
     if (comm->comm && g_rccl.destroy) {
+        if (int e = set_device(comm->ctx)) rc = e;
         if (int e = g_rccl.destroy(comm->comm)) rc = rccl_fail("ncclCommDestroy", e);
     }
     delete comm;

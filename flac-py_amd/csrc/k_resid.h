@@ -571,10 +571,11 @@ __device__ __forceinline__ void mf8_tile_epilogue(const v4i (&D)[4], int s, cons
  * 4, 2, 6, 1, 5, 3, 7.  After each tier from the second on, every wave reads the workgroup's exact partial LPC sums (a sum
  * over a subset of the values, so a lower bound of each order's full sum) against the best
  * exact fixed sum; once every order's partial sum exceeds it, LPC can neither win nor tie
- * (encoder.py:135-157) and the remaining tiers are skipped: returns true (workgroup-uniform;
- * red then holds partial LPC sums).  Otherwise the four tiers add up to the exact sums. */
+ * (encoder.py:135-157) and the remaining tiers are skipped (red then holds partial LPC
+ * sums).  Otherwise the eight tiers add up to the exact sums.  Returns (workgroup-uniform)
+ * the eighths done | 0x100 if pruned, or 0 without pruning. */
 template <int LMAX>
-__device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const unsigned char* pl, int PLB,
+__device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const unsigned char* pl, int PLB,
                                                    const int32_t* cfl, const int32_t* lsh, int L, int n, int G,
                                                    int tid, int NT, int lane, int wid, int nw,
                                                    unsigned long long* red, bool prune) {
@@ -761,9 +762,10 @@ __device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const un
     if (!prune) {
         go(wid, nw);
         store();
-        return false;
+        return 0;
     }
     bool pruned = false;
+    int done = 0;
     /* eighths of the wave's tiles, spread over the block (residues 0, 4, 2, 6, 1, 5, 3, 7 of
      * the wave's tile index mod 8): a unit stops at the first eighth whose partial LPC sums
      * all exceed the best fixed sum (config 3: LPC sums run ~4x the fixed ones, so most
@@ -780,6 +782,7 @@ __device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const un
             go(wid + res * nw, kTiers * nw);
         }
         store();
+        done = t + 1;
         if (t == kTiers - 1) break; /* every tile done: the sums are exact */
         __syncthreads();
         uint64_t tj = 0;
@@ -796,7 +799,7 @@ __device__ __forceinline__ bool mf8_candidate_sums(const int32_t* xs32, const un
         __syncthreads(); /* every wave has read red before the next tier stores */
         if (pruned) break;
     }
-    return pruned;
+    return done | (pruned ? 0x100 : 0);
 }
 
 /* Phase E of the fast kernel for a fixed predictor of order K (encoder.py:331-359,
@@ -1049,6 +1052,7 @@ next_unit:
     const int PLB = mf8_plane_bytes(n);
     uint32_t* mf8_xmax = reinterpret_cast<uint32_t*>(smem + lay.coef + CT::TAPF_OFF); /* [nw] */
     bool use_mf8 = false, lpc_pruned = false;
+    int lpc_tiers = 0; /* meta.lpc_tiers */
     int mf8_G = 0;
     int16_t* xs16 = reinterpret_cast<int16_t*>(smem + lay.xs) + HP; /* [-HP, npad) (S16) */
     int32_t* xs32 = reinterpret_cast<int32_t*>(smem + lay.xs) + HP; /* [-HP, npad) (others) */
@@ -1428,8 +1432,12 @@ next_unit:
         if (a.stop_after == 2) goto unit_done;
     } else if (MF8 && use_mf8) {
         if constexpr (MF8)
-            lpc_pruned = mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
-                                                  nw, red, a.prune != 0 && !lpc_only && !rice_only);
+        {
+            const int r = mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
+                                                   nw, red, a.prune != 0 && !lpc_only && !rice_only);
+            lpc_pruned = (r >> 8) != 0;
+            lpc_tiers = r ? (r & 0xff) | (8 << 8) : 0;
+        }
         if (a.stop_after == 2) goto unit_done;
     } else if constexpr (!FAST) {
     A acc[NSUM];
@@ -1560,6 +1568,7 @@ next_unit:
             dec->ncoefs = ncoefs;
             dec->fixed_order = fo;
             dec->lpc_order = lbest;
+            dec->tiers = lpc_tiers;
             dec->fixed_sum = (long long)fsum;
             dec->lpc_sum = (long long)lsum;
         }
@@ -2037,7 +2046,7 @@ next_unit:
 #pragma unroll
             for (int o = 0; o < 16; ++o) tb[o] += tp[o];
             if (a.stop_after == 7) { /* ablation: after the data bits (kept live) */
-                if (tb[0] == 0x9e3779b9u) meta->reserved0 = 1;
+                if (tb[0] == 0x9e3779b9u) meta->lpc_tiers = 1;
                 goto unit_done;
             }
             {

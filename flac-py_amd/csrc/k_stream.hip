@@ -274,7 +274,7 @@ __device__ __forceinline__ void lpc_chunk(const uint16_t* xs, int i0, int32_t co
  * coefs[lane - 20] from lane q's `coef`. */
 struct MetaVals {
     int status, site, kind, order, shift, ncoefs, res_offset, res_len, fixed_order, lpc_order, part_order,
-        n_parts, coding;
+        n_parts, coding, tiers;
     long long fixed_sum, lpc_sum, rice_bits;
 };
 __device__ __forceinline__ void store_meta(flacmi_unit_meta* m, int lane, const MetaVals& v, int32_t coef) {
@@ -282,7 +282,7 @@ __device__ __forceinline__ void store_meta(flacmi_unit_meta* m, int lane, const 
     const uint32_t f[20] = {(uint32_t)v.status, (uint32_t)v.site, (uint32_t)v.kind, (uint32_t)v.order,
                             (uint32_t)v.shift, (uint32_t)v.ncoefs, (uint32_t)v.res_offset, (uint32_t)v.res_len,
                             (uint32_t)v.fixed_order, (uint32_t)v.lpc_order, (uint32_t)v.part_order,
-                            (uint32_t)v.n_parts, (uint32_t)v.coding, 0u, (uint32_t)v.fixed_sum,
+                            (uint32_t)v.n_parts, (uint32_t)v.coding, (uint32_t)v.tiers, (uint32_t)v.fixed_sum,
                             (uint32_t)((unsigned long long)v.fixed_sum >> 32), (uint32_t)v.lpc_sum,
                             (uint32_t)((unsigned long long)v.lpc_sum >> 32), (uint32_t)v.rice_bits,
                             (uint32_t)((unsigned long long)v.rice_bits >> 32)};
@@ -605,6 +605,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                     const uint64_t lb = tj > (uint64_t)n ? tj - (uint64_t)n : 0ull;
                     const uint64_t open = __ballot(lane >= 16 && lane < 16 + L && lb <= fmin);
                     pruned = open == 0 || a.stop_after >= 11; /* 11, 12: ablation, tier 0 only */
+                    mv.tiers = t | (4 << 8);
                     if (pruned || t == 4) break;
                     /* the next quarter of the blocks (k % 4 == 2, 1, 3; block 0 is in tier 0), only
                      * for the groups that hold an undecided order (mostly order 1's) */
@@ -626,6 +627,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                     tj = lane_total();
                 }
                 if (!pruned) { /* rare: the exact LPC sums over every block */
+                    mv.tiers = 5 | (4 << 8);
                     __syncthreads(); /* every wave has read the bounds */
 #pragma unroll
                     for (int g = 1; g <= NG; ++g) acc[g] = 0;
@@ -944,7 +946,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         for (int i = 0; i < FLACMI_PAD_VALU / 8; ++i)
             asm volatile("v_add_u32 %0, %0, %4\n v_add_u32 %1, %1, %4\n v_add_u32 %2, %2, %4\n v_add_u32 %3, %3, %4"
                          : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3) : "v"(lane));
-        if ((q0 ^ q1 ^ q2 ^ q3) == 0xdeadbeefu) meta->reserved0 = 1;
+        if ((q0 ^ q1 ^ q2 ^ q3) == 0xdeadbeefu) meta->lpc_tiers = 1;
     }
 #endif
 #if defined(FLACMI_PAD_SALU) /* diagnostic build only: extra SALU per unit */
@@ -953,7 +955,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
 #pragma unroll
         for (int i = 0; i < FLACMI_PAD_SALU / 4; ++i)
             asm volatile("s_add_u32 %0, %0, 3\n s_add_u32 %1, %1, 5" : "+s"(q0), "+s"(q1));
-        if ((q0 ^ q1) == 0xdeadbeefu) meta->reserved0 = 1;
+        if ((q0 ^ q1) == 0xdeadbeefu) meta->lpc_tiers = 1;
     }
 #endif
     if (wid != 0) return;

@@ -13,6 +13,7 @@ single-unit forms of the same device analysis, returning the reference's datacla
 import collections
 import concurrent.futures
 import functools
+import threading
 from dataclasses import dataclass
 from typing import Iterator, Optional, Sequence
 
@@ -213,7 +214,7 @@ def encode(sample_rate: int, sample_size: int, channels: int, frames: int,
         if pending:
             yield index, functools.partial(_planar, pending, channels, n)
 
-    yield from _drive(batches(), _sessions(device, devices), params, n, channels, sample_size)
+    yield from _drive(batches(), lambda: _sessions(device, devices), params, n, channels, sample_size)
 
 
 def encode_planar(sample_rate: int, sample_size: int, pcm: np.ndarray, parameters: EncoderParameters, *,
@@ -239,7 +240,7 @@ def encode_planar(sample_rate: int, sample_size: int, pcm: np.ndarray, parameter
         for b0 in range(0, nb, bpb):
             yield b0, functools.partial(planar_blocks, pcm, n, b0, bpb)
 
-    yield from _drive(batches(), _sessions(device, devices), params, n, channels, sample_size)
+    yield from _drive(batches(), lambda: _sessions(device, devices), params, n, channels, sample_size)
 
 
 def encode_wav(path, parameters: EncoderParameters, *, quirk: bool = True, device: int = 0,
@@ -333,61 +334,84 @@ class _Session:
             return data.tobytes(), offsets, status
 
 
-_SESSIONS = {}
+_IDLE = collections.defaultdict(list)   # device -> sessions no running encode holds
+_IDLE_LOCK = threading.Lock()
 
 
 def _sessions(device: int, devices: Optional[Sequence[int]]):
-    """One cached session per entry of devices (an entry repeated: another context on that
-    device)."""
-    out = []
-    seen = {}
-    for d in (list(devices) if devices else [device]):
-        k = (int(d), seen.get(int(d), 0))
-        seen[int(d)] = k[1] + 1
-        if k not in _SESSIONS:
-            _SESSIONS[k] = _Session(int(d))
-        out.append(_SESSIONS[k])
-    if not out:
+    """Check out one session per entry of devices (an entry repeated: another context on
+    that device).  A session belongs to one _drive call at a time: its staging slots are
+    written by the generator while its worker copies the previous batch from them, so two
+    generators on one device (interleaved, or on two threads) get two sessions.  _drive
+    returns them when it finishes or is closed."""
+    ds = [int(d) for d in (list(devices) if devices else [device])]
+    if not ds:
         raise ValueError("devices is empty")
+    with _IDLE_LOCK:
+        out = [_IDLE[d].pop() if _IDLE[d] else None for d in ds]
+    try:
+        for k, d in enumerate(ds):
+            if out[k] is None:
+                out[k] = _Session(d)
+    except BaseException:
+        _release([s for s in out if s is not None])
+        raise
     return out
+
+
+def _release(sessions) -> None:
+    with _IDLE_LOCK:
+        for s in sessions:
+            _IDLE[s.az.device].append(s)
 
 
 def _drive(batches, sessions, params, n, channels, sample_size) -> Iterator[bytes]:
     """batches yields (first_block, cut) with cut(alloc=...) -> (rows, bits, tail_len,
     n_tail_units); batch i goes to sessions[i % D].  Frames are yielded in block order; a
     frame the reference would fail on raises its exception after the frames before it, and
-    an exception from `batches` itself (the WAV reader) after every earlier batch's frames."""
+    an exception from `batches` itself (the WAV reader) after every earlier batch's frames.
+    sessions (a list from _sessions, or a callable returning one) are held until the
+    generator ends or is closed, after every queued batch has finished with them."""
     queue = collections.deque()
     failure = None
     it = iter(batches)
+    held = None
     i = 0
-    while True:
-        try:
-            item = next(it)
-        except StopIteration:
-            break
-        except Exception as e:  # the reader's failure surfaces in stream order
-            failure = e
-            break
-        if callable(sessions):
-            sessions = sessions()
-        D = len(sessions)
-        while len(queue) >= 2 * D:  # batch i reuses the staging slot of batch i - 2D
+    try:
+        while True:
+            try:
+                item = next(it)
+            except StopIteration:
+                break
+            except Exception as e:  # the reader's failure surfaces in stream order
+                failure = e
+                break
+            if held is None:
+                held = sessions() if callable(sessions) else sessions
+            D = len(held)
+            while len(queue) >= 2 * D:  # batch i reuses the staging slot of batch i - 2D
+                yield from _frames(*queue.popleft().result())
+            first_block, cut = item
+            s, slot = held[i % D], (i // D) % 2
+            try:
+                rows, bits, tail_len, n_tail = cut(alloc=functools.partial(s.staging, slot))
+            except Exception as e:
+                failure = e
+                break
+            queue.append(s.pool.submit(s.encode, rows, bits, tail_len, n_tail, params, n, channels, sample_size,
+                                       first_block))
+            i += 1
+        while queue:
             yield from _frames(*queue.popleft().result())
-        first_block, cut = item
-        s, slot = sessions[i % D], (i // D) % 2
-        try:
-            rows, bits, tail_len, n_tail = cut(alloc=functools.partial(s.staging, slot))
-        except Exception as e:
-            failure = e
-            break
-        queue.append(s.pool.submit(s.encode, rows, bits, tail_len, n_tail, params, n, channels, sample_size,
-                                   first_block))
-        i += 1
-    while queue:
-        yield from _frames(*queue.popleft().result())
-    if failure is not None:
-        raise failure
+        if failure is not None:
+            raise failure
+    finally:
+        for f in queue:  # closed early: the workers may still read the staging slots
+            concurrent.futures.wait([f])
+        if held is not None:
+            _release(held)
+        elif not callable(sessions):
+            _release(sessions)
 
 
 def _frames(buf: bytes, offsets: np.ndarray, status: np.ndarray) -> Iterator[bytes]:

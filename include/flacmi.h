@@ -41,7 +41,10 @@
 extern "C" {
 #endif
 
-#define FLACMI_ABI_VERSION 1
+/* 2: in the default (pruning) mode meta.lpc_order / meta.lpc_sum of a unit whose LPC
+      candidates provably lose read FLACMI_LPC_PRUNED, and stats word 80 no longer folds
+      lpc_sum (round 3); version 1 callers read exact LPC fields there */
+#define FLACMI_ABI_VERSION 2
 #define FLACMI_MAX_LPC_ORDER 32      /* EncoderParameters: lpc_order.stop <= 33 (encoder.py:42) */
 #define FLACMI_MAX_BLOCK 65535       /* largest block the reference writes (encoder.py:249-253, 16-bit uncommon
                                         code); analysis returns FLACMI_E_UNSUPPORTED where a block's
@@ -170,7 +173,10 @@ typedef struct flacmi_unit_meta {
     int32_t part_order;      /* Residual.partition_order as chosen by rice_partitions */
     int32_t n_parts;         /* len(Residual.partitions) */
     int32_t coding_method;   /* RiceCodingMethod value: 4 or 5 */
-    int32_t reserved0;
+    int32_t lpc_tiers;       /* diagnostic, the pruning decision: LPC candidate passes made | passes of the
+                                path << 8.  16-bit stream kernel: quarter-block bound passes 1..4, then 5 =
+                                the exact pass; int8-MFMA path: eighths 2..8 of exact partial sums (8 = every
+                                tile).  0 where no pruning runs (fixed-only, all-candidates, other paths) */
     int64_t fixed_sum;       /* sum(|r|) of the best fixed residual */
     int64_t lpc_sum;         /* sum(|r|) of the best LPC residual (0 in fixed-only mode, FLACMI_LPC_PRUNED if pruned) */
     int64_t rice_bits;       /* size estimate of the chosen partitioning (encoder.py:714-727) */

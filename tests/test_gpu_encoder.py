@@ -174,3 +174,32 @@ def test_encode_planar_multi_context_and_frame_error_order(enc):
         for f in enc.encode_planar(44100, 16, bad, p, blocks_per_batch=2, devices=[0, 0]):
             got.append(f)
     assert got == one[:3 + 5]
+
+
+def test_interleaved_generators_do_not_share_staging(enc):
+    """Two encode_planar generators on one device consumed in turn (zip), and two threads
+    encoding at once: each stream equals its own sequential run byte for byte (each _drive
+    call checks out its own session and staging slots)."""
+    import concurrent.futures
+    p = enc.EncoderParameters(block_size=4608, rice_partition_order=range(0, 6),
+                              lpc_order=range(0, 13), qlp_precision=5)
+    a = np.array([_sine(4608 * 12)], dtype=np.int64)
+    b = np.array([[((v * 7) % 20001) - 10000 for v in range(4608 * 12)]], dtype=np.int64)
+    seq_a = list(enc.encode_planar(44100, 16, a, p, blocks_per_batch=1))
+    seq_b = list(enc.encode_planar(44100, 16, b, p, blocks_per_batch=1))
+    assert seq_a != seq_b
+    za, zb = [], []
+    for fa, fb in zip(enc.encode_planar(44100, 16, a, p, blocks_per_batch=1),
+                      enc.encode_planar(44100, 16, b, p, blocks_per_batch=1)):
+        za.append(fa)
+        zb.append(fb)
+    assert za == seq_a and zb == seq_b
+    with concurrent.futures.ThreadPoolExecutor(2) as ex:
+        fa = ex.submit(lambda: list(enc.encode_planar(44100, 16, a, p, blocks_per_batch=1)))
+        fb = ex.submit(lambda: list(enc.encode_planar(44100, 16, b, p, blocks_per_batch=1)))
+        assert fa.result() == seq_a and fb.result() == seq_b
+    # a generator closed early hands its session back
+    g = enc.encode_planar(44100, 16, a, p, blocks_per_batch=1)
+    next(g), next(g), next(g), next(g)
+    g.close()
+    assert list(enc.encode_planar(44100, 16, a, p, blocks_per_batch=1)) == seq_a

@@ -47,7 +47,7 @@ def _equal(a, b, key, k):
     for u in range(k):
         pruned = int(ma[u]["lpc_order"]) == abi.LPC_PRUNED or int(mb[u]["lpc_order"]) == abi.LPC_PRUNED
         for f in abi.META_DTYPE.names:
-            if f == "reserved0" or (pruned and f in ("lpc_order", "lpc_sum")):
+            if f == "lpc_tiers" or (pruned and f in ("lpc_order", "lpc_sum")):
                 continue
             assert np.array_equal(ma[u][f], mb[u][f]), (key, u, f, ma[u][f], mb[u][f])
         if int(ma[u]["status"]) != 0:

@@ -437,7 +437,7 @@ def _meta_params_residual_equal(a, b, u):
     am, bm = a["meta"], b["meta"]
     pruned = int(am["lpc_order"][u]) == abi.LPC_PRUNED
     for f in abi.META_DTYPE.names:
-        if f == "reserved0" or (pruned and f in ("lpc_order", "lpc_sum")):
+        if f == "lpc_tiers" or (pruned and f in ("lpc_order", "lpc_sum")):
             continue
         assert np.array_equal(am[f][u], bm[f][u]), (u, f, am[f][u], bm[f][u])
     if pruned:
@@ -550,6 +550,16 @@ def test_lpc_pruning_paths_vs_oracle(az, q):
     pruned = pm["lpc_order"] == abi.LPC_PRUNED
     if q == 5:  # (at q >= 9 these units exceed k_resid_stream's MFMA bound: k_resid never prunes)
         assert pruned[:24].sum() >= 12, "config-2 units should mostly prune"
+    # meta.lpc_tiers: k_resid_stream's quarter bound passes 1..4 (pruned) or 5 (the exact
+    # pass); 0 for units its retry list redid on k_resid (no pruning there)
+    tiers = pm["lpc_tiers"].astype(np.int64)
+    st = tiers != 0
+    assert (tiers[st] >> 8 == 4).all()
+    assert (pruned[st] == ((tiers[st] & 0xff) <= 4)).all()
+    assert ((tiers[st] & 0xff) <= 5).all() and ((tiers[st] & 0xff) >= 1).all()
+    assert not pruned[~st].any()
+    if q == 5:
+        assert (tiers == (1 | 4 << 8)).any() and (tiers == (5 | 4 << 8)).any(), np.unique(tiers)
     assert (ok & ~pruned & (om["kind"] == abi.KIND_FIXED)).any(), "no unit took the exact pass and chose fixed"
     assert (ok & (om["kind"] == abi.KIND_LPC)).any(), "no LPC-chosen unit"
 
@@ -572,3 +582,130 @@ def test_production_batches_vs_oracle(az, cfg):
     pruned = out["meta"]["lpc_order"] == abi.LPC_PRUNED
     assert pruned.mean() > 0.9, pruned.mean()
     assert (ora["meta"]["kind"][pruned] == abi.KIND_FIXED).all()
+
+
+# ---------------------------------------------------------------------------------------
+# config-3 production mode: the int8-MFMA path's LPC pruning tiers (k_resid.h
+# mf8_candidate_sums) against the oracle, with the tier that decided each unit
+# ---------------------------------------------------------------------------------------
+def _resid_threads_wide(n):
+    """device_common.h resid_threads(n, wide=true): k_resid's workgroup on the 64-bit paths."""
+    nch = (n + 7) // 8
+    nt = 64 * ((nch + 64 * 3 - 1) // (64 * 3))
+    return max(64, min(nt, 512))
+
+
+def _lpc_abs_tiles(x, rec, p):
+    """|r| of LPC order p (encoder.py:537-548) from the oracle's record, summed per 16-sample
+    tile, zero below the candidate's first residual (p, or 0 in the negative-shift branch)."""
+    n = len(x)
+    x64 = x.astype(np.int64)
+    r = np.zeros(n, np.int64)
+    if (int(rec[1]) >> (p - 1)) & 1:  # ([], 0): the residual is the samples
+        r = np.abs(x64)
+    else:
+        sh = int(rec[2 + p - 1])
+        c = rec[2 + 32 + p * (p - 1) // 2: 2 + 32 + p * (p - 1) // 2 + p].astype(np.int64)
+        pred = np.zeros(n - p, np.int64)
+        for j in range(p):
+            pred += c[j] * x64[p - 1 - j: n - 1 - j]
+        r[p:] = np.abs(x64[p:] - (pred >> sh))
+    return r.reshape(-1, 16).sum(1)
+
+
+def _emulate_eighths(x, rec, L, fixed_sums):
+    """The pruning decision of mf8_candidate_sums restated on the oracle's record: wave w
+    of nw owns tiles w + k nw; the eighths run residues {0, 4}, 2, 6, 1, 5, 3, 7 of k mod 8;
+    after each, the unit is pruned when every order's exact partial sum exceeds the best
+    fixed sum (encoder.py:135-157: LPC can then neither win nor tie).  -> (eighths, pruned)."""
+    ntile = len(x) // 16
+    k = np.arange(ntile) // (_resid_threads_wide(len(x)) // 64)
+    per = np.array([_lpc_abs_tiles(x, rec, p) for p in range(1, L + 1)])
+    fmin = int(np.min(fixed_sums))
+    mask = np.zeros(ntile, bool)
+    done = 0
+    for res in ((0, 4), (2,), (6,), (1,), (5,), (3,), (7,)):
+        for r_ in res:
+            mask |= (k % 8) == r_
+        done += len(res)
+        if done < 8 and (per[:, mask].sum(1) > fmin).all():
+            return done, True
+    return 8, False
+
+
+def _c3_tier_units(n, q):
+    """24-bit units on every side of the eighth-tier decision (explored with
+    _emulate_eighths): full-scale tones at noise 0 / 0.5 / 4 and config-3 synthetic units
+    (pruned after two eighths, some after three to six), AR(1) noise (LPC ~1.3x fixed:
+    pruned after six or seven), weak AR(1) and white noise (every eighth, then fixed or LPC
+    wins), small white noise (LPC within a few units of fixed: near ties) and, at n = 4096,
+    units whose best LPC and fixed sums are equal (the tie AssertionError, encoder.py:157)."""
+    rng = np.random.default_rng(n + q)
+    rows = [_tones24(3, n, 1, 0.0), _tones24(3, n, 2, 0.5), _tones24(3, n, 3, 4.0),
+            oracle.synth_batch(0, 6, n, 24, 11, dtype=np.int32)]
+    x = []
+    for u in range(4):
+        w = rng.normal(0, 2e5, n)
+        a = w.copy()
+        a[1:] += (0.9 if u % 2 else -0.7) * w[:-1]
+        x.append(a)
+    for u in range(4):
+        w = rng.normal(0, 2e5, n)
+        a = w.copy()
+        a[1:] += (0.4 + 0.05 * u) * w[:-1]
+        x.append(a)
+    for u in range(6):
+        w = rng.normal(0, 2e5, n)
+        a = w.copy()
+        a[1:] += 0.02 * (u - 3) * w[:-1]
+        x.append(a)
+    rows.append(np.clip(np.round(np.array(x)), -2 ** 23, 2 ** 23 - 1).astype(np.int32))
+    rows.append(rng.integers(-2 ** 22, 2 ** 22, (4, n)).astype(np.int32))
+    rows.append(rng.integers(-300, 300, (8, n)).astype(np.int32))
+    if n == 4096:  # searched with the oracle: an exact tie of the best fixed and LPC sums
+        for seed, u in ({15: ((15002, 440), (15003, 1)), 12: ((12003, 138), (12003, 461))}[q]):
+            rows.append(np.random.default_rng(seed).integers(-300, 300, (512, n)).astype(np.int32)[u:u + 1])
+    return np.ascontiguousarray(np.concatenate(rows))
+
+
+@pytest.mark.parametrize("q", [15, 12])
+@pytest.mark.parametrize("n", [16384, 4096])
+def test_c3_int8_pruning_tiers_vs_oracle(az, n, q):
+    """Config-3 production mode (LPC pruning on) on the int8-MFMA path, 24-bit, L = 32,
+    r 0..8: every reference-visible field equals the oracle and the all-candidates run, and
+    meta.lpc_tiers (the eighths computed before the decision) equals the decision restated
+    on the oracle's exact candidates.  Each outcome occurs: pruned after two eighths, pruned
+    later, every eighth then fixed, LPC chosen, a near tie, and (n = 4096) the tie
+    AssertionError (encoder.py:133-157)."""
+    L = 32
+    a = _c3_tier_units(n, q)
+    nu = len(a)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, 8), n, sample_bits=24, threads=16)
+    prod = az.analyze(a, make_params(L, q, 0, 8), n, sample_bits=24)
+    full = az.analyze(a, make_params(L, q, 0, 8, all_candidates=True), n, sample_bits=24)
+    compare_with_oracle(prod, ora, [n] * nu)
+    compare_with_oracle(full, ora, [n] * nu)
+    assert (full["meta"]["lpc_tiers"] == 0).all()
+    pm, om = prod["meta"], ora["meta"]
+    seen = set()
+    for u in range(nu):
+        _meta_params_residual_equal(prod, full, u)
+        st = int(om["status"][u])
+        if st != 0 and int(om["site"][u]) != abi.SITE_CHOICE_TIE:
+            continue
+        done, pr = _emulate_eighths(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u])
+        tiers = int(pm["lpc_tiers"][u])
+        assert tiers == done | (8 << 8), (u, "lpc_tiers", tiers & 0xff, tiers >> 8, "want", done)
+        assert (int(pm["lpc_order"][u]) == abi.LPC_PRUNED) == pr, (u, "pruned")
+        if st != 0:
+            seen.add("tie")
+        elif pr:
+            seen.add("pruned@2" if done == 2 else "pruned-later")
+        elif int(om["kind"][u]) == abi.KIND_LPC:
+            seen.add("lpc")
+        else:
+            seen.add("exact-fixed")
+        if st == 0 and not pr and abs(int(om["lpc_sum"][u]) - int(om["fixed_sum"][u])) <= 1e-3 * int(om["fixed_sum"][u]):
+            seen.add("near-tie")
+    want = {"pruned@2", "pruned-later", "exact-fixed", "lpc", "near-tie"} | ({"tie"} if n == 4096 else set())
+    assert want <= seen, want - seen

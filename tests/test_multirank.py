@@ -113,6 +113,7 @@ def test_bench_self_launches_n_ranks(gpus, config):
     assert d["rank_mask"] == (1 << gpus) - 1
     assert d["units_total"] == d["expected_units"]
     assert d["elapsed_max"] == pytest.approx(0.001 * gpus)
+    assert d["comm_id_broadcast_ok"] is True  # rank 0's comm id reached every rank
 
 
 def test_bench_rejects_world_size_mismatch():
@@ -133,3 +134,22 @@ def test_shard_plan_round_robin_chunks():
             assert total == 10_500 and all(c % world == r for c in chunks)
             seen += chunks
         assert sorted(seen) == list(range(11))
+
+
+def test_reduce_stats_routes_through_the_c_abi_comm():
+    """With a C-ABI communicator bench.reduce_stats calls its allreduce_stats on the stats
+    buffer and the launch stream (flacmi_allreduce_stats), not torch.distributed."""
+    import torch
+    sys.path.insert(0, REPO)
+    import bench
+
+    class Comm:
+        calls = []
+
+        def allreduce_stats(self, ptr, stream):
+            self.calls.append((ptr, stream))
+
+    st = torch.zeros(128, dtype=torch.int64)
+    c = Comm()
+    assert bench.reduce_stats(st, None, c, 1234) is st
+    assert c.calls == [(st.data_ptr(), 1234)]
