@@ -100,20 +100,26 @@ def check_world(args, world):
 
 
 def algorithmic_bytes(cfg, meta_np, n_units):
-    """Bytes the analysis must move per batch: samples in, zig-zag residuals (4 B) +
-    per-unit results (meta, Rice parameters) out; the k_lpc -> k_resid LPC record
-    crosses HBM too.  Per kernel:
-      k_lpc  : n*s_in (samples) + 4*rec_words (record)
-      k_resid: n*s_in + 4*rec_words + 4*(n - order) + 208 (meta) + 4*n_parts"""
+    """SURVEY §8d algorithmic bytes per batch, B = n*s_in + 4*(n - order) + M per unit with
+    M = 16 + 4*2^rmax + 4*L (samples in, the chosen zig-zag residual and the metadata out),
+    per kernel:
+      k_lpc  : n*s_in (it reads the samples; its LPC record is workspace)
+      k_resid: B (samples in, residual + metadata out)
+      step   : B (the whole analysis call)
+    and, labelled separately, the same with the k_lpc -> k_resid LPC record (4 * rec_words:
+    intermediate workspace, not SURVEY bytes) and this build's real metadata (208 B meta +
+    4 B per Rice parameter)."""
     s_in = 2 if cfg["bits"] <= 16 else 4
     n = cfg["n"]
     rec = 4 * (2 + cfg["L"] + cfg["L"] * (cfg["L"] + 1) // 2) if cfg["mode"] == 0 else 0
     res = 4.0 * float(meta_np["res_len"].mean())
     parts = 4.0 * float(meta_np["n_parts"].mean())
-    lpc = n_units * (n * s_in + rec)
-    resid = n_units * (n * s_in + rec + res + 208 + parts)
-    pipeline = n_units * (n * s_in + res + 208 + parts)
-    return lpc, resid, pipeline
+    m_survey = 16 + 4 * (1 << cfg["rmax"]) + 4 * cfg["L"]
+    survey = {"k_lpc": n_units * n * s_in, "k_resid": n_units * (n * s_in + res + m_survey),
+              "step": n_units * (n * s_in + res + m_survey)}
+    workspace = {"k_lpc": n_units * (n * s_in + rec), "k_resid": n_units * (n * s_in + rec + res + 208 + parts),
+                 "step": n_units * (n * s_in + res + 208 + parts)}
+    return survey, workspace
 
 
 def _host_cpus():
@@ -594,12 +600,14 @@ def main(argv=None):
     if rank == 0 and world == 1 and args.e2e_units > 0 and not chunked and not os.environ.get("FLACMI_DEBUG_STOP"):
         e2e = end_to_end_leg(args, cfg, az)
 
-    lpc_b, resid_b, pipe_b = algorithmic_bytes(cfg, meta_np, units)
+    ab, ab_ws = algorithmic_bytes(cfg, meta_np, units)
+    lpc_b, resid_b, pipe_b = ab["k_lpc"], ab["k_resid"], ab["step"]
     lpc_gbs = lpc_b / (kt["lpc_ms"] * 1e-3) / 1e9 if kt["lpc_ms"] > 0 else 0.0
     resid_gbs = resid_b / (kt["resid_ms"] * 1e-3) / 1e9 if kt["resid_ms"] > 0 else 0.0
     dominant = "k_resid" if kt["resid_ms"] >= kt["lpc_ms"] else "k_lpc"
     dom_gbs = resid_gbs if dominant == "k_resid" else lpc_gbs
     dom_bytes = resid_b if dominant == "k_resid" else lpc_b
+    dom_ms = kt["resid_ms"] if dominant == "k_resid" else kt["lpc_ms"]
     traffic = None
     tfile = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tfile):  # HBM bytes per launch from the separate rocprofv3 --pmc passes
@@ -634,6 +642,13 @@ def main(argv=None):
                          "traffic_source": (os.path.relpath(tfile, REPO) + ": rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                                             "of this config (tools/profile.sh, tools/traffic.py)") if traffic else None,
                          "algorithmic_bytes_per_launch": dom_bytes,
+                         "algorithmic_bytes_source": "SURVEY §8d: n*s_in + 4*(n - order) + 16 + 4*2^rmax + 4*L per unit",
+                         "kernel_ms": dom_ms,
+                         # labelled separately: with the k_lpc -> k_resid LPC record (workspace)
+                         # and this build's 208-byte meta + Rice parameters
+                         "with_workspace": {"bytes_per_launch": ab_ws[dominant],
+                                            "frac": ab_ws[dominant] / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                            if dom_ms else None},
                          # the whole analysis step (k_lpc + k_resid + retries): SURVEY 8d bytes / call time
                          "pipeline_frac": (pipe_b / (kt["call_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS) if kt["call_ms"] else None,
                          "pipeline_algorithmic_bytes": pipe_b},

@@ -18,17 +18,129 @@ __device__ __forceinline__ void write_quant(int32_t* rec, int L, int p, const in
         if (j < p) c[j] = j < nq ? q[j] : 0;
 }
 
+/* Levinson-Durbin at max order with a snapshot per order (encoder.py:453-479), each
+ * snapshot quantised (encoder.py:482-534), into the unit's LPC record */
+template <int LMAX>
+__device__ __forceinline__ void lpc_finish(const double (&acc)[LMAX + 1], const LpcArgs& a, int32_t* __restrict__ rec) {
+    const int L = a.L, q = a.q;
+    const pym::PowTables PT{c_log_hdr, c_log_tab, c_exp_hdr, c_exp_tab};
+    double c[LMAX + 1];
+    c[0] = 1.0;
+#pragma unroll
+    for (int j = 1; j <= LMAX; ++j) c[j] = 0.0;
+    double err = acc[0];
+    int lst = ST_OK, lsite = 0, qst = ST_OK, qsite = 0;
+    uint32_t negmask = 0;
+    const double qmax = (double)((1LL << (q - 1)) - 1);
+    const double qmin = -(double)(1LL << (q - 1));
+    static_for<LMAX>([&](auto K_) {
+        constexpr int k = K_;
+        if (k < L && lst == ST_OK) {
+            double lam = 0.0;
+#pragma unroll
+            for (int j = 0; j <= k; ++j) lam = lam - c[j] * acc[k + 1 - j];
+            if (err == 0.0) {
+                lst = ST_ZERODIV;
+                lsite = FLACMI_SITE_LEVINSON_DIV;
+            } else {
+                lam = lam / err;
+#pragma unroll
+                for (int nn = 0; nn <= (k + 1) / 2; ++nn) {
+                    const double tmp = c[k + 1 - nn] + lam * c[nn];
+                    c[nn] = c[nn] + lam * c[k + 1 - nn];
+                    c[k + 1 - nn] = tmp;
+                }
+                int pst;
+                const double l2 = pym::py_pow2(lam, PT, &pst);
+                if (pst) {
+                    lst = ST_OVERFLOW;
+                    lsite = FLACMI_SITE_LEVINSON_POW;
+                } else {
+                    err = err * (1.0 - l2);
+                }
+            }
+            /* quantise order p = k + 1 (encoder.py:482-534) unless an earlier order failed */
+            if (lst == ST_OK && qst == ST_OK) {
+                const int p = k + 1;
+                double cm = __builtin_fabs(c[1]);
+#pragma unroll
+                for (int j = 2; j <= LMAX; ++j)
+                    if (j <= p && __builtin_fabs(c[j]) > cm) cm = __builtin_fabs(c[j]);
+                int32_t qv[LMAX];
+                int nq = 0, shift = 0;
+                if (!(cm > 0.0)) {
+                    qst = ST_ASSERT;
+                    qsite = FLACMI_SITE_QUANT_CMAX;
+                } else if (__builtin_isinf(cm)) {
+                    qst = ST_OVERFLOW;
+                    qsite = FLACMI_SITE_QUANT_LOG2;
+                } else {
+                    shift = q - pym::py_floor_log2(cm, a.log2thr) - 2;
+                    if (shift > 15) shift = 15;
+                    if (shift < -16) {
+                        qst = ST_ASSERT;
+                        qsite = FLACMI_SITE_QUANT_SHIFT;
+                    } else {
+                        const bool neg = shift < 0;
+                        const double scale = pow2_exact(neg ? -shift : shift);
+                        double e = 0.0;
+#pragma unroll
+                        for (int j = 1; j <= LMAX; ++j) {
+                            if (j <= p && qst == ST_OK) {
+                                e = e + c[j] * scale;
+                                if (__builtin_isinf(e)) {
+                                    qst = ST_OVERFLOW;
+                                    qsite = FLACMI_SITE_QUANT_ROUND_INF;
+                                } else if (__builtin_isnan(e)) {
+                                    qst = ST_VALUE;
+                                    qsite = FLACMI_SITE_QUANT_ROUND_NAN;
+                                } else {
+                                    const double r = __builtin_rint(e);
+                                    const double qq = r < qmin ? qmin : (r > qmax ? qmax : r);
+                                    e = e - qq;
+                                    qv[j - 1] = (int32_t)qq;
+                                }
+                            }
+                        }
+                        if (qst == ST_OK) {
+                            if (neg) {
+                                negmask |= 1u << k;
+                                shift = 0;
+                                nq = 0;
+                            } else {
+                                nq = p;
+                            }
+                            write_quant<LMAX>(rec, L, p, qv, nq, shift);
+                        }
+                    }
+                }
+            }
+        }
+    });
+    int st = lst != ST_OK ? lst : qst;
+    int site = lst != ST_OK ? lsite : qsite;
+    if (st == ST_OK && L == 0) { /* min() over no candidates (encoder.py:404) */
+        st = ST_VALUE;
+        site = FLACMI_SITE_LPC_EMPTY;
+    }
+    rec[0] = st | (site << 16);
+    rec[1] = (int32_t)negmask;
+}
+
 /* ACF_IN: the autocorrelation is read from a.acf ([count][33]) instead of computed from
  * samples -- the entry point flacmi_device_lpc_from_acf uses to drive Levinson-Durbin and
  * the quantiser into the overflow sites integer PCM never reaches. */
+/* three waves per SIMD for the common orders (L <= 12: <= 168 VGPRs) */
+constexpr int lpc_waves(int lmax) { return lmax <= 12 ? 3 : 1; }
+
 template <int LMAX, typename SampleT, bool ACF_IN = false>
-__global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(LMAX)))) void k_lpc(LpcArgs a) {
     const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (gid >= a.count) return;
     const int64_t u = a.unit0 + gid;
     const SampleT* __restrict__ x = (const SampleT*)a.samples + u * a.stride;
     int32_t* __restrict__ rec = a.rec + gid * a.rec_words;
-    const int n = a.n, L = a.L, q = a.q;
+    const int n = a.n, L = a.L;
 
     constexpr int S = ((LMAX + 1 + 7) / 8) * 8;
     double acc[LMAX + 1];
@@ -187,114 +299,165 @@ __global__ __launch_bounds__(256) void k_lpc(LpcArgs a) {
     }
     } /* !ACF_IN */
 
-    /* ---- Levinson-Durbin at max order with a snapshot per order (encoder.py:453-479) ---- */
-    const pym::PowTables PT{c_log_hdr, c_log_tab, c_exp_hdr, c_exp_tab};
-    double c[LMAX + 1];
-    c[0] = 1.0;
+    lpc_finish<LMAX>(acc, a, rec);
+}
+
+
+/* k_lpc_tile: the same per-lane chains (and lpc_finish) for int16 samples at L <= 12, with
+ * the samples staged through LDS in whole 128-byte lines: per 64-sample tile each wave
+ * copies its 64 rows' lines with eight global_load_lds_dwordx4 (one instruction = 8 rows x
+ * 128 B, DMA straight into LDS), each lane then reads its row's 128 B into registers and
+ * the wave issues the next tile's copies at once, so they land behind this tile's f64
+ * work.  k_lpc's own loads are lane-strided (64 rows per 16-byte instruction: every
+ * instruction touches 64 lines, and a line's two halves arrive 32 samples apart, when L2
+ * may have dropped it).
+ * LDS image of a wave (8 KB): slot 8 r + j (16 B) holds segment (j + r) & 7 of row r, so the
+ * lanes reading segment k of their own rows hit 16 distinct 16-byte columns per quarter
+ * wave (no bank conflicts); the DMA writes lane-linearly, so the rotation is applied to the
+ * per-lane SOURCE address. */
+template <int LMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(LMAX)))) void k_lpc_tile(LpcArgs a) {
+    __shared__ __align__(16) uint4 tiles[4 * 512];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t wave0 = (int64_t)blockIdx.x * 256 + wid * 64;
+    if (wave0 >= a.count) return; /* wave-uniform; the host launches whole waves (count % 64 == 0) */
+    const int64_t gid = wave0 + lane;
+    const int n = a.n, L = a.L;
+    int32_t* __restrict__ rec = a.rec + gid * a.rec_words;
+    constexpr int S = ((LMAX + 1 + 7) / 8) * 8;
+    static_assert(32 % S == 0, "ring length divides a half tile");
+    double acc[LMAX + 1];
+    if (n >= 4 && n <= 7) { /* tukey: nr == 0 -> pi * 0 / 0 (encoder.py:437) */
+        rec[0] = ST_ZERODIV | (FLACMI_SITE_TUKEY << 16);
+        rec[1] = 0;
+        if (a.acf)
+            for (int l = 0; l < 33; ++l) a.acf[gid * 33 + l] = 0.0;
+        return;
+    }
+    double ring[S];
 #pragma unroll
-    for (int j = 1; j <= LMAX; ++j) c[j] = 0.0;
-    double err = acc[0];
-    int lst = ST_OK, lsite = 0, qst = ST_OK, qsite = 0;
-    uint32_t negmask = 0;
-    const double qmax = (double)((1LL << (q - 1)) - 1);
-    const double qmin = -(double)(1LL << (q - 1));
-    static_for<LMAX>([&](auto K_) {
-        constexpr int k = K_;
-        if (k < L && lst == ST_OK) {
-            double lam = 0.0;
+    for (int t = 0; t < S; ++t) ring[t] = 0.0;
 #pragma unroll
-            for (int j = 0; j <= k; ++j) lam = lam - c[j] * acc[k + 1 - j];
-            if (err == 0.0) {
-                lst = ST_ZERODIV;
-                lsite = FLACMI_SITE_LEVINSON_DIV;
-            } else {
-                lam = lam / err;
+    for (int l = 0; l <= LMAX; ++l) acc[l] = 0.0;
+    const int M = n - 1; /* the last sample never enters a product (encoder.py:449) */
+    /* the window through the constant address space: scalar loads (a generic pointer read
+     * beside the LDS-DMA intrinsic is loaded per lane and waited for with vmcnt(0), which
+     * would also wait for the next tile's copies) */
+    const __attribute__((address_space(4))) double* win = (const __attribute__((address_space(4))) double*)a.window;
+    const int ntile = (M + 63) >> 6;
+    uint4* tile = tiles + 512 * wid;
+    /* the DMA source of lane l in copy j: row 8 j + l / 8, segment (l % 8 + l / 8) % 8 of the
+     * tile, clamped to the row's stride (a clamped segment lies at or past n, whose samples
+     * the tile masks) */
+    const int seg = ((lane & 7) + (lane >> 3)) & 7;
+    const int smax = (int)a.stride - 8;
+    const int16_t* row0 = (const int16_t*)a.samples + (a.unit0 + wave0 + (lane >> 3)) * a.stride;
+    const int64_t rstep = 8 * a.stride; /* elements from copy j to j + 1 (wave-uniform) */
+    auto issue = [&](int m0) __attribute__((always_inline)) {
+        int off = m0 + 8 * seg;
+        off = off < smax ? off : smax;
+        const int16_t* p = row0 + off;
 #pragma unroll
-                for (int nn = 0; nn <= (k + 1) / 2; ++nn) {
-                    const double tmp = c[k + 1 - nn] + lam * c[nn];
-                    c[nn] = c[nn] + lam * c[k + 1 - nn];
-                    c[k + 1 - nn] = tmp;
-                }
-                int pst;
-                const double l2 = pym::py_pow2(lam, PT, &pst);
-                if (pst) {
-                    lst = ST_OVERFLOW;
-                    lsite = FLACMI_SITE_LEVINSON_POW;
-                } else {
-                    err = err * (1.0 - l2);
+        for (int j = 0; j < 8; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(p + j * rstep),
+                                             (void __attribute__((address_space(3)))*)(tile + 64 * j), 16, 0, 0);
+    };
+    /* this lane's row in the image: segment k at slot 8 lane + ((k - lane) & 7) */
+    const uint4* myrow = tile + 8 * lane;
+    const int rot = (-lane) & 7;
+    if (ntile > 0) issue(0);
+    for (int tI = 0; tI < ntile; ++tI) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* this wave's copies have landed */
+        /* two halves of 32 samples; the next tile's copies go out once the second half is
+         * read out of the image (they land behind its f64 work) */
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int m0 = (tI << 6) + 32 * h;
+            uint32_t v[16];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 q = myrow[(4 * h + k + rot) & 7];
+                v[4 * k] = q.x, v[4 * k + 1] = q.y, v[4 * k + 2] = q.z, v[4 * k + 3] = q.w;
+            }
+            if (h == 1) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* read out before the copies overwrite it */
+                if (tI + 1 < ntile) issue((tI + 1) << 6);
+            }
+            if (m0 + 32 > M) { /* the last samples: those >= M are zero, as k_lpc loads them */
+#pragma unroll
+                for (int w = 0; w < 16; ++w) {
+                    const int m = m0 + 2 * w;
+                    v[w] = m >= M ? 0u : (m + 1 >= M ? (v[w] & 0xffffu) : v[w]);
                 }
             }
-            /* quantise order p = k + 1 (encoder.py:482-534) unless an earlier order failed */
-            if (lst == ST_OK && qst == ST_OK) {
-                const int p = k + 1;
-                double cm = __builtin_fabs(c[1]);
 #pragma unroll
-                for (int j = 2; j <= LMAX; ++j)
-                    if (j <= p && __builtin_fabs(c[j]) > cm) cm = __builtin_fabs(c[j]);
-                int32_t qv[LMAX];
-                int nq = 0, shift = 0;
-                if (!(cm > 0.0)) {
-                    qst = ST_ASSERT;
-                    qsite = FLACMI_SITE_QUANT_CMAX;
-                } else if (__builtin_isinf(cm)) {
-                    qst = ST_OVERFLOW;
-                    qsite = FLACMI_SITE_QUANT_LOG2;
+            for (int sb = 0; sb < 32 / S; ++sb) {
+                const int ms = m0 + sb * S;
+                if (ms - LMAX >= a.fuse_lo && ms + S <= a.fuse_hi) {
+                    /* inside the Tukey rectangle: exact integer products, one FMA per term (k_lpc) */
+#pragma unroll
+                    for (int t = 0; t < S; ++t) {
+                        const int i = sb * S + t;
+                        const double av = (double)((i & 1) ? (int32_t)v[i >> 1] >> 16 : (int32_t)(v[i >> 1] << 16) >> 16);
+                        ring[t] = av;
+#pragma unroll
+                        for (int l = 0; l <= LMAX; ++l) acc[l] = __builtin_fma(ring[(t - l + S) % S], av, acc[l]);
+                    }
                 } else {
-                    shift = q - pym::py_floor_log2(cm, a.log2thr) - 2;
-                    if (shift > 15) shift = 15;
-                    if (shift < -16) {
-                        qst = ST_ASSERT;
-                        qsite = FLACMI_SITE_QUANT_SHIFT;
-                    } else {
-                        const bool neg = shift < 0;
-                        const double scale = pow2_exact(neg ? -shift : shift);
-                        double e = 0.0;
 #pragma unroll
-                        for (int j = 1; j <= LMAX; ++j) {
-                            if (j <= p && qst == ST_OK) {
-                                e = e + c[j] * scale;
-                                if (__builtin_isinf(e)) {
-                                    qst = ST_OVERFLOW;
-                                    qsite = FLACMI_SITE_QUANT_ROUND_INF;
-                                } else if (__builtin_isnan(e)) {
-                                    qst = ST_VALUE;
-                                    qsite = FLACMI_SITE_QUANT_ROUND_NAN;
-                                } else {
-                                    const double r = __builtin_rint(e);
-                                    const double qq = r < qmin ? qmin : (r > qmax ? qmax : r);
-                                    e = e - qq;
-                                    qv[j - 1] = (int32_t)qq;
-                                }
-                            }
-                        }
-                        if (qst == ST_OK) {
-                            if (neg) {
-                                negmask |= 1u << k;
-                                shift = 0;
-                                nq = 0;
-                            } else {
-                                nq = p;
-                            }
-                            write_quant<LMAX>(rec, L, p, qv, nq, shift);
+                    for (int t = 0; t < S; ++t) {
+                        const int i = sb * S + t;
+                        const double av =
+                            (double)((i & 1) ? (int32_t)v[i >> 1] >> 16 : (int32_t)(v[i >> 1] << 16) >> 16) * win[ms + t];
+                        ring[t] = av;
+#pragma unroll
+                        for (int l = 0; l <= LMAX; ++l) {
+                            const double prev = ring[(t - l + S) % S];
+                            acc[l] = acc[l] + prev * av;
                         }
                     }
                 }
             }
         }
-    });
-    int st = lst != ST_OK ? lst : qst;
-    int site = lst != ST_OK ? lsite : qsite;
-    if (st == ST_OK && L == 0) { /* min() over no candidates (encoder.py:404) */
-        st = ST_VALUE;
-        site = FLACMI_SITE_LPC_EMPTY;
     }
-    rec[0] = st | (site << 16);
-    rec[1] = (int32_t)negmask;
+    if (a.acf) {
+        double* o = a.acf + gid * 33;
+#pragma unroll
+        for (int l = 0; l < 33; ++l) o[l] = (l <= LMAX && l <= L) ? acc[l < LMAX ? l : LMAX] : 0.0;
+    }
+    lpc_finish<LMAX>(acc, a, rec);
+}
+
+/* FLACMI_LPC_TILE=0 selects k_lpc for int16 rows (A/B and parity comparison) */
+static bool lpc_tile_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FLACMI_LPC_TILE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 template <int LMAX>
 static hipError_t launch_lpc_T(const LpcArgs& a, hipStream_t s) {
     const dim3 grid((unsigned)((a.count + 255) / 256));
+    if constexpr (LMAX <= 12) {
+        /* whole waves of rows made of whole 16-byte segments (the tile's clamp stays inside
+         * the row) through k_lpc_tile; the last count % 64 units through k_lpc */
+        const int64_t full = a.count & ~(int64_t)63;
+        if (a.sample_bytes == 2 && lpc_tile_enabled() && a.stride % 8 == 0 && a.stride >= 8 && full > 0) {
+            LpcArgs t = a;
+            t.count = full;
+            hipLaunchKernelGGL((k_lpc_tile<LMAX>), dim3((unsigned)((full + 255) / 256)), dim3(256), 0, s, t);
+            if (full == a.count) return hipGetLastError();
+            LpcArgs r = a;
+            r.unit0 += full;
+            r.count = a.count - full;
+            r.rec += full * a.rec_words;
+            if (r.acf) r.acf += full * 33;
+            hipLaunchKernelGGL((k_lpc<LMAX, int16_t>), dim3((unsigned)((r.count + 255) / 256)), dim3(256), 0, s, r);
+            return hipGetLastError();
+        }
+    }
     if (a.sample_bytes == 2)
         hipLaunchKernelGGL((k_lpc<LMAX, int16_t>), grid, dim3(256), 0, s, a);
     else

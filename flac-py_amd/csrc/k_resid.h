@@ -578,7 +578,7 @@ template <int LMAX>
 __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const unsigned char* pl, int PLB,
                                                    const int32_t* cfl, const int32_t* lsh, int L, int n, int G,
                                                    int tid, int NT, int lane, int wid, int nw,
-                                                   unsigned long long* red, bool prune) {
+                                                   unsigned long long* red, bool prune, int dbg) {
     using CT = CoefTables<LMAX>;
     constexpr int NSUM = 5 + LMAX;
     constexpr int NTMAX = (LMAX + 15) / 16;
@@ -763,6 +763,15 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
         go(wid, nw);
         store();
         return 0;
+    }
+    /* ablation (timing only, FLACMI_DEBUG_STOP): 13 fixed sums alone, 14 the first quarter of
+     * the LPC tiles without the tier test, 15 every LPC tile without tier tests; each then
+     * reports the unit pruned */
+    if (dbg == 13) return 0x100;
+    if (dbg == 14 || dbg == 15) {
+        go(wid, dbg == 14 ? 4 * nw : nw);
+        store();
+        return 0x100 | (dbg == 14 ? 2 : 8);
     }
     bool pruned = false;
     int done = 0;
@@ -1434,7 +1443,7 @@ next_unit:
         if constexpr (MF8)
         {
             const int r = mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
-                                                   nw, red, a.prune != 0 && !lpc_only && !rice_only);
+                                                   nw, red, a.prune != 0 && !lpc_only && !rice_only, a.stop_after);
             lpc_pruned = (r >> 8) != 0;
             lpc_tiers = r ? (r & 0xff) | (8 << 8) : 0;
         }

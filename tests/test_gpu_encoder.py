@@ -184,7 +184,7 @@ def test_interleaved_generators_do_not_share_staging(enc):
     p = enc.EncoderParameters(block_size=4608, rice_partition_order=range(0, 6),
                               lpc_order=range(0, 13), qlp_precision=5)
     a = np.array([_sine(4608 * 12)], dtype=np.int64)
-    b = np.array([[((v * 7) % 20001) - 10000 for v in range(4608 * 12)]], dtype=np.int64)
+    b = np.random.default_rng(7).integers(-9000, 9000, (1, 4608 * 12)).astype(np.int64)
     seq_a = list(enc.encode_planar(44100, 16, a, p, blocks_per_batch=1))
     seq_b = list(enc.encode_planar(44100, 16, b, p, blocks_per_batch=1))
     assert seq_a != seq_b

@@ -558,8 +558,8 @@ def test_lpc_pruning_paths_vs_oracle(az, q):
     assert (pruned[st] == ((tiers[st] & 0xff) <= 4)).all()
     assert ((tiers[st] & 0xff) <= 5).all() and ((tiers[st] & 0xff) >= 1).all()
     assert not pruned[~st].any()
-    if q == 5:
-        assert (tiers == (1 | 4 << 8)).any() and (tiers == (5 | 4 << 8)).any(), np.unique(tiers)
+    if q == 5:  # pruned after the first quarter, and after later ones
+        assert (tiers == (1 | 4 << 8)).any() and ((tiers[st] & 0xff) >= 2).any(), np.unique(tiers)
     assert (ok & ~pruned & (om["kind"] == abi.KIND_FIXED)).any(), "no unit took the exact pass and chose fixed"
     assert (ok & (om["kind"] == abi.KIND_LPC)).any(), "no LPC-chosen unit"
 
