@@ -574,7 +574,7 @@ __device__ __forceinline__ void mf8_tile_epilogue(const v4i (&D)[4], int s, cons
  * (encoder.py:135-157) and the remaining tiers are skipped (red then holds partial LPC
  * sums).  Otherwise the eight tiers add up to the exact sums.  Returns (workgroup-uniform)
  * the eighths done | 0x100 if pruned, or 0 without pruning. */
-template <int LMAX>
+template <int LMAX, bool PIPE = true>
 __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const unsigned char* pl, int PLB,
                                                    const int32_t* cfl, const int32_t* lsh, int L, int n, int G,
                                                    int tid, int NT, int lane, int wid, int nw,
@@ -694,6 +694,29 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
      * tile's MFMAs are never used). */
     auto run = [&](auto NTL_, int T, const int step) __attribute__((always_inline)) {
         constexpr int NTL = decltype(NTL_)::value;
+        if constexpr (!PIPE) { /* one register set (kVarMf8: four waves per SIMD hide the latencies) */
+            Mf8Raw r0, r1, r2;
+            v4i D[NTL][4];
+            for (; T < 2 && T < ntile; T += step) { /* masked */
+                mf8_load(pw0 + 4 * T, r0);
+                mf8_load(pw1 + 4 * T, r1);
+                mf8_load(pw2 + 4 * T, r2);
+                mm(r0, r1, r2, D);
+                ep(D, T, std::true_type{});
+            }
+            flush();
+            int g = 0;
+            for (; T < ntile; T += step) {
+                mf8_load(pw0 + 4 * T, r0);
+                mf8_load(pw1 + 4 * T, r1);
+                mf8_load(pw2 + 4 * T, r2);
+                mm(r0, r1, r2, D);
+                ep(D, T, std::false_type{});
+                if (++g == G) flush(), g = 0;
+            }
+            flush();
+            return;
+        }
         Mf8Raw a0, a1, a2, b0, b1, b2;
         v4i DA[NTL][4], DB[NTL][4];
         while (T < 2 && T < ntile) {
@@ -1010,20 +1033,32 @@ __device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta
  *                outside the MFMA exactness bound is marked FLACMI_STATUS_RETRY and listed;
  *   kVarList     units retry_list[li], li = blockIdx.x, blockIdx.x + gridDim.x, ... below
  *                *retry_count, every path. */
-enum { kVarGeneric = 0, kVarFast = 1, kVarList = 2 };
+enum { kVarGeneric = 0, kVarFast = 1, kVarList = 2, kVarMf8 = 3, kVarList1 = 4 };
+/* kVarMf8 (PATH_W64, LMAX >= 16): only the int8-MFMA path, fixed-predictor choice and the
+ * wide Rice step, in 1024-thread workgroups (four waves per SIMD instead of two: the unit's
+ * 140 KB of LDS allows one workgroup per CU either way); a unit that needs anything else
+ * (outside the int8 bounds, an LPC or order > 4 choice, another Rice shape) is marked
+ * FLACMI_STATUS_RETRY and listed for kVarList1: the 512-thread generic body, one workgroup
+ * per unit of the batch, retry_list[blockIdx.x] below *retry_count (no unit loop: the
+ * looping list variant of the 64-bit path spills) */
+__host__ __device__ constexpr int resid_launch_bound(int path, int lmax, int var) {
+    return var == kVarMf8 ? 1024 : path >= PATH_W64 ? 512 : 256;
+}
 template <int LMAX, int PATH, typename ResT, int VAR>
-__global__ __launch_bounds__(PATH >= PATH_W64 ? 512 : 256) void k_resid(ResidArgs a) {
+__global__ __launch_bounds__(resid_launch_bound(PATH, LMAX, VAR)) void k_resid(ResidArgs a) {
     constexpr bool FAST = VAR == kVarFast;
+    constexpr bool M8V = VAR == kVarMf8;
+    static_assert(!M8V || (PATH == PATH_W64 && LMAX >= 16 && sizeof(ResT) == 4), "kVarMf8: int8-MFMA units only");
     /* the list variant (units another kernel handed over) loops over the list with a small
      * grid (kListGrid) instead of a workgroup per unit of the batch: a million near-empty
      * workgroups cost ~0.3 ms of dispatch at config 2.  Every exit of the body is
      * workgroup-uniform, so each one goes to the next listed unit. */
     int64_t li = blockIdx.x, gid = blockIdx.x;
-    if constexpr (VAR == kVarList) {
+    if constexpr (VAR == kVarList || VAR == kVarList1) {
         if (li >= (int64_t)*a.retry_count) return;
     }
 next_unit:
-    if constexpr (VAR == kVarList) gid = a.retry_list[li];
+    if constexpr (VAR == kVarList || VAR == kVarList1) gid = a.retry_list[li];
     {
     using UX = ResT;
     constexpr bool S16 = PATH == PATH_S16;
@@ -1079,6 +1114,14 @@ next_unit:
     double* tl = reinterpret_cast<double*>(smem + lay.tl); /* log2 thresholds, e in [kTlLo, kTlLo+64) */
     flacmi_unit_meta* meta = a.meta + gid;
     const int32_t* __restrict__ rec = ref_mode ? a.rec + gid * a.rec_words : nullptr;
+    /* kVarMf8: hand the unit to the list variant (workgroup-uniform callers) */
+    auto list_unit = [&]() __attribute__((always_inline)) {
+        if (tid == 0) {
+            meta->status = FLACMI_STATUS_RETRY;
+            const unsigned long long k = atomicAdd(a.retry_count, 1ull);
+            a.retry_list[k] = gid;
+        }
+    };
 
     /* ---- phase A: stage samples and the candidate coefficients ---- */
     uint32_t sumx = 0; /* this thread's sum|x| (MFMA path: the fixed order-0 sum) */
@@ -1424,6 +1467,12 @@ next_unit:
         }
     }
     if (a.stop_after == 1) goto unit_done;
+    if constexpr (M8V) {
+        if (!use_mf8) { /* outside the int8 bounds: the int64 chains of the list variant */
+            list_unit();
+            goto unit_done;
+        }
+    }
 
     /* ---- phase B: sum|r| for fixed orders 0..4 and LPC orders 1..L ---- */
     if (FAST && !use_mfma) { /* outside the MFMA exactness bound: the generic kernel redoes it */
@@ -1442,13 +1491,13 @@ next_unit:
     } else if (MF8 && use_mf8) {
         if constexpr (MF8)
         {
-            const int r = mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
+            const int r = mf8_candidate_sums<LMAX, !M8V>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
                                                    nw, red, a.prune != 0 && !lpc_only && !rice_only, a.stop_after);
             lpc_pruned = (r >> 8) != 0;
             lpc_tiers = r ? (r & 0xff) | (8 << 8) : 0;
         }
         if (a.stop_after == 2) goto unit_done;
-    } else if constexpr (!FAST) {
+    } else if constexpr (!FAST && !M8V) {
     A acc[NSUM];
 #pragma unroll
     for (int s = 0; s < NSUM; ++s) acc[s] = 0;
@@ -1793,6 +1842,12 @@ next_unit:
     /* int8-MFMA units (|x| <= 2^23) that chose a fixed predictor: int32 difference chains */
     const int wfk = __builtin_amdgcn_readfirstlane(
         (MF8 && use_mf8 && dec->kind == FLACMI_KIND_FIXED && order <= 4) ? order : -1);
+    if constexpr (M8V) {
+        if (wfk < 0 || wr_om < 0) { /* an LPC (or order > 4) choice, or another Rice shape */
+            list_unit();
+            goto unit_done;
+        }
+    }
     auto wide_pass = [&](auto kk) __attribute__((always_inline)) {
     constexpr int KK = decltype(kk)::value;
 #pragma unroll 1
@@ -1831,7 +1886,9 @@ next_unit:
             case 2: wide_pass(std::integral_constant<int, 2>{}); break;
             case 3: wide_pass(std::integral_constant<int, 3>{}); break;
             case 4: wide_pass(std::integral_constant<int, 4>{}); break;
-            default: wide_pass(std::integral_constant<int, -1>{}); break;
+            default:
+                if constexpr (!M8V) wide_pass(std::integral_constant<int, -1>{});
+                break;
         }
     } else {
         wide_pass(std::integral_constant<int, -1>{});
@@ -2111,6 +2168,7 @@ next_unit:
             goto unit_done;
         }
     }
+    if constexpr (!M8V) {
     /* finest partition sums: heap nodes [P, 2P); zz[i] = 0 for i < start */
     for (int k = wid; k < P; k += nw) {
         const int lo = k * ps, hi = (k + 1) * ps;
@@ -2247,6 +2305,7 @@ next_unit:
     const int best = misc[3];
     int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
     for (int K = tid; K < (1 << best); K += NT) rp[K] = hp[(1 << best) + K];
+    } /* !M8V */
     } /* !FAST */
     }
 unit_done:
@@ -2336,9 +2395,48 @@ static inline bool resid_fast_ok(const ResidArgs& a) {
            resid_regz(a.n, rmax_eff, true) && (a.n + 7) / 8 + 1 >= a.rec_words;
 }
 
+/* FLACMI_MF8_1024=1: config-3 shapes through kVarMf8 (opt-in while it is measured) */
+static inline bool mf8_1024_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("FLACMI_MF8_1024");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+/* kVarMf8 over the batch (1024 threads per unit), then the 512-thread list variant over the
+ * units it listed */
+template <int LMAX>
+static hipError_t launch_resid_mf8(const ResidArgs& a, hipStream_t s) {
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (a.n % (1 << o) == 0) rmax_eff = o;
+    const int P = 1 << (rmax_eff < 0 ? 0 : rmax_eff);
+    const int nt8 = 1024, ntl = resid_threads(a.n, true);
+    const size_t lds8 = resid_lds_layout(LMAX, a.n, nt8 / 64, P, 4, 4, CoefTables<LMAX>::BYTES, false, true).total;
+    const size_t ldsl = resid_lds_layout(LMAX, a.n, ntl / 64, P, 4, 4, CoefTables<LMAX>::BYTES, false, true).total;
+    hipError_t e = hipMemsetAsync(a.retry_count, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    auto k8 = k_resid<LMAX, PATH_W64, uint32_t, kVarMf8>;
+    if ((e = hipFuncSetAttribute((const void*)k8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(k8, dim3((unsigned)a.count), dim3(nt8), lds8, s, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_poison_lds(s)) != hipSuccess) return e;
+    auto kl = k_resid<LMAX, PATH_W64, uint32_t, kVarList1>;
+    if ((e = hipFuncSetAttribute((const void*)kl, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsl)) != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(kl, dim3((unsigned)a.count), dim3(ntl), ldsl, s, a);
+    return hipGetLastError();
+}
+
 template <int LMAX>
 static hipError_t launch_resid_bucket(const ResidArgs& a, int path, int rb, hipStream_t s) {
     if (rb == 8) return launch_resid_T<LMAX, PATH_W64, uint64_t>(a, s);
+    if constexpr (LMAX >= 16)
+        if (path == PATH_W64 && a.mode == FLACMI_MODE_REFERENCE && a.mfma && a.retry_list && a.retry_count &&
+            a.sample_bytes == 4 && a.L >= 1 && a.n % 16 == 0 && a.n >= 8192 && mf8_1024_enabled())
+            return launch_resid_mf8<LMAX>(a, s);
     if constexpr (LMAX == 8 || LMAX == 12)
         if (path == PATH_S16 && resid_fast_ok(a)) return launch_resid_fast<LMAX>(a, s);
     if (path == PATH_S16) return launch_resid_T<LMAX, PATH_S16, uint32_t>(a, s);

@@ -589,7 +589,11 @@ def test_production_batches_vs_oracle(az, cfg):
 # mf8_candidate_sums) against the oracle, with the tier that decided each unit
 # ---------------------------------------------------------------------------------------
 def _resid_threads_wide(n):
-    """device_common.h resid_threads(n, wide=true): k_resid's workgroup on the 64-bit paths."""
+    """device_common.h resid_threads(n, wide=true): k_resid's workgroup on the 64-bit paths
+    (1024 threads: k_resid.h kVarMf8, which FLACMI_MF8_1024=1 selects for n >= 8192)."""
+    import os
+    if os.environ.get("FLACMI_MF8_1024") == "1" and n >= 8192 and n % 16 == 0:
+        return 1024
     nch = (n + 7) // 8
     nt = 64 * ((nch + 64 * 3 - 1) // (64 * 3))
     return max(64, min(nt, 512))
@@ -611,6 +615,25 @@ def _lpc_abs_tiles(x, rec, p):
             pred += c[j] * x64[p - 1 - j: n - 1 - j]
         r[p:] = np.abs(x64[p:] - (pred >> sh))
     return r.reshape(-1, 16).sum(1)
+
+
+def _int8_path(x, rec, L):
+    """Whether k_resid runs the unit's candidate sums on int8 MFMA (k_resid.h, phase A's
+    bound): every sample's top balanced digit fits a byte (x <= 8355711), every coefficient's
+    top digit too (c in [-32640, 32639]), and B = max|x| + max_p (sum|c_p| max|x| >> s_p) + 1 <
+    2^29.  Otherwise the exact int64 chains run, without pruning."""
+    xa = x.astype(np.int64)
+    if int(xa.max()) > 8355711:
+        return False
+    xm = int(np.abs(xa).max())
+    b = 0
+    for p in range(1, L + 1):
+        c = rec[2 + 32 + p * (p - 1) // 2: 2 + 32 + p * (p - 1) // 2 + p].astype(np.int64)
+        if (c > 32639).any() or (c < -32640).any():
+            return False
+        sa = int(np.abs(c).sum()) & 0xFFFFFFFF
+        b = max(b, xm + ((sa * xm) >> int(rec[2 + p - 1])) + 1)
+    return b < (1 << 29)
 
 
 def _emulate_eighths(x, rec, L, fixed_sums):
@@ -693,8 +716,12 @@ def test_c3_int8_pruning_tiers_vs_oracle(az, n, q):
         st = int(om["status"][u])
         if st != 0 and int(om["site"][u]) != abi.SITE_CHOICE_TIE:
             continue
-        done, pr = _emulate_eighths(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u])
         tiers = int(pm["lpc_tiers"][u])
+        if not _int8_path(a[u], ora["lpc_records"][u], L):  # the int64 chains: exact, no pruning
+            assert tiers == 0 and int(pm["lpc_order"][u]) != abi.LPC_PRUNED, (u, "int64 path", tiers)
+            seen.add("int64")
+            continue
+        done, pr = _emulate_eighths(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u])
         assert tiers == done | (8 << 8), (u, "lpc_tiers", tiers & 0xff, tiers >> 8, "want", done)
         assert (int(pm["lpc_order"][u]) == abi.LPC_PRUNED) == pr, (u, "pruned")
         if st != 0:
