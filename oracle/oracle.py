@@ -144,7 +144,7 @@ def meta_mismatches(dev, ora) -> list:
     bad = []
     pruned = int(dev["lpc_order"]) == abi.LPC_PRUNED
     for f in abi.META_DTYPE.names:
-        if f in ("coefs", "reserved0") or (pruned and f in ("lpc_order", "lpc_sum")):
+        if f in ("coefs", "lpc_tiers") or (pruned and f in ("lpc_order", "lpc_sum")):
             continue
         if dev[f] != ora[f]:
             bad.append((f, dev[f], ora[f]))
