@@ -662,7 +662,11 @@ def main(argv=None):
             "parity": parity,
             "stream_stats": {"units": int(st[0]), "samples": int(st[1]), "rice_bits": int(st[2]),
                              "fixed": int(st[3]), "lpc": int(st[4]), "lpc_pruned": int(st[81]),
-                             "errors": int(st[65:80].sum())},
+                             "errors": int(st[65:80].sum()),
+                             # meta.lpc_tiers of this rank's last batch: LPC candidate passes made
+                             # before the decision, as "passes/passes of the path": units
+                             "lpc_tiers": {f"{t & 0xff}/{t >> 8}": int(c) for t, c in
+                                           zip(*np.unique(meta_np["lpc_tiers"], return_counts=True))}},
         }
         print(json.dumps(line), flush=True)
     if comm is not None:

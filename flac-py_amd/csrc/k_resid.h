@@ -529,12 +529,23 @@ __device__ __forceinline__ void mf8_digits(int32_t x, int32_t& b0, int32_t& b1, 
     b2 = (x1 - b1) >> 8;
 }
 
-/* a 16-byte window of a plane at any byte alignment: the five dwords that cover it (read
- * one tile ahead), then four v_alignbyte by the window's byte offset within the first */
+/* a 16-byte window of a plane at any byte alignment (tile T of the lane's window starts 16 T
+ * bytes after p): one unaligned ds_read_b128 (gfx950 reads LDS at any byte address), or with
+ * -DFLACMI_MF8_ALIGNBYTE the five dwords that cover it and four v_alignbyte by its offset */
+#ifndef FLACMI_MF8_ALIGNBYTE
+struct Mf8Raw {
+    v4i v;
+};
+__device__ __forceinline__ void mf8_load(const unsigned char* p, int T, Mf8Raw& r) {
+    __builtin_memcpy(&r.v, p + 16 * T, 16);
+}
+__device__ __forceinline__ v4i mf8_align(const Mf8Raw& r, uint32_t) { return r.v; }
+#else
 struct Mf8Raw {
     uint32_t d[5];
 };
-__device__ __forceinline__ void mf8_load(const uint32_t* pw, Mf8Raw& r) {
+__device__ __forceinline__ void mf8_load(const unsigned char* p, int T, Mf8Raw& r) {
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(p - (reinterpret_cast<uintptr_t>(p) & 3)) + 4 * T;
 #pragma unroll
     for (int k = 0; k < 5; ++k) r.d[k] = pw[k];
 }
@@ -544,6 +555,7 @@ __device__ __forceinline__ v4i mf8_align(const Mf8Raw& r, uint32_t sh) {
     for (int k = 0; k < 4; ++k) v[k] = (int)__builtin_amdgcn_alignbyte(r.d[k + 1], r.d[k], sh);
     return v;
 }
+#endif
 
 /* one 16-sample tile for N-tile operands B*, accumulating |r| of the lane's column into s32 */
 template <bool MASK>
@@ -646,14 +658,13 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
     /* the lane's three windows: plane 0; plane 1 (slot 0) or 0 (slot 1); plane 2 or 1.  A
      * tile start is a multiple of 16 samples, so each window's byte alignment is fixed and
      * tile T reads dwords 4T further on. */
-    const uint32_t* pw = reinterpret_cast<const uint32_t*>(pl);
     const int off0 = kMf8Pad + m - 16 - 16 * h;
     const int off1 = off0 + (sg == 0 ? PLB : 0);
     const int off2 = off0 + (sg == 0 ? 2 * PLB : PLB);
     const uint32_t al = (uint32_t)(off0 & 3); /* PLB is a multiple of 16 */
-    const uint32_t* pw0 = pw + (off0 >> 2);
-    const uint32_t* pw1 = pw + (off1 >> 2);
-    const uint32_t* pw2 = pw + (off2 >> 2);
+    const unsigned char* pw0 = pl + off0;
+    const unsigned char* pw1 = pl + off1;
+    const unsigned char* pw2 = pl + off2;
     const v4i Z{0, 0, 0, 0};
     uint64_t acc[NTMAX];
     uint32_t s32[NTMAX];
@@ -698,18 +709,18 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
             Mf8Raw r0, r1, r2;
             v4i D[NTL][4];
             for (; T < 2 && T < ntile; T += step) { /* masked */
-                mf8_load(pw0 + 4 * T, r0);
-                mf8_load(pw1 + 4 * T, r1);
-                mf8_load(pw2 + 4 * T, r2);
+                mf8_load(pw0, T, r0);
+                mf8_load(pw1, T, r1);
+                mf8_load(pw2, T, r2);
                 mm(r0, r1, r2, D);
                 ep(D, T, std::true_type{});
             }
             flush();
             int g = 0;
             for (; T < ntile; T += step) {
-                mf8_load(pw0 + 4 * T, r0);
-                mf8_load(pw1 + 4 * T, r1);
-                mf8_load(pw2 + 4 * T, r2);
+                mf8_load(pw0, T, r0);
+                mf8_load(pw1, T, r1);
+                mf8_load(pw2, T, r2);
                 mm(r0, r1, r2, D);
                 ep(D, T, std::false_type{});
                 if (++g == G) flush(), g = 0;
@@ -720,30 +731,30 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
         Mf8Raw a0, a1, a2, b0, b1, b2;
         v4i DA[NTL][4], DB[NTL][4];
         while (T < 2 && T < ntile) {
-            mf8_load(pw0 + 4 * T, a0);
-            mf8_load(pw1 + 4 * T, a1);
-            mf8_load(pw2 + 4 * T, a2);
+            mf8_load(pw0, T, a0);
+            mf8_load(pw1, T, a1);
+            mf8_load(pw2, T, a2);
             mm(a0, a1, a2, DA);
             ep(DA, T, std::true_type{});
             T += step;
         }
         flush();
         if (T >= ntile) return;
-        mf8_load(pw0 + 4 * T, a0);
-        mf8_load(pw1 + 4 * T, a1);
-        mf8_load(pw2 + 4 * T, a2);
+        mf8_load(pw0, T, a0);
+        mf8_load(pw1, T, a1);
+        mf8_load(pw2, T, a2);
         mm(a0, a1, a2, DA);
         int Tn = T + step < ntile ? T + step : T;
-        mf8_load(pw0 + 4 * Tn, b0);
-        mf8_load(pw1 + 4 * Tn, b1);
-        mf8_load(pw2 + 4 * Tn, b2);
+        mf8_load(pw0, Tn, b0);
+        mf8_load(pw1, Tn, b1);
+        mf8_load(pw2, Tn, b2);
         int g = 0;
         for (;;) {
             int Tnn = Tn + step < ntile ? Tn + step : Tn;
             mm(b0, b1, b2, DB);
-            mf8_load(pw0 + 4 * Tnn, a0);
-            mf8_load(pw1 + 4 * Tnn, a1);
-            mf8_load(pw2 + 4 * Tnn, a2);
+            mf8_load(pw0, Tnn, a0);
+            mf8_load(pw1, Tnn, a1);
+            mf8_load(pw2, Tnn, a2);
             ep(DA, T, std::false_type{});
             T += step;
             if (++g == G) flush(), g = 0;
@@ -751,9 +762,9 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
             Tn = Tnn;
             Tnn = Tn + step < ntile ? Tn + step : Tn;
             mm(a0, a1, a2, DA);
-            mf8_load(pw0 + 4 * Tnn, b0);
-            mf8_load(pw1 + 4 * Tnn, b1);
-            mf8_load(pw2 + 4 * Tnn, b2);
+            mf8_load(pw0, Tnn, b0);
+            mf8_load(pw1, Tnn, b1);
+            mf8_load(pw2, Tnn, b2);
             ep(DB, T, std::false_type{});
             T += step;
             if (++g == G) flush(), g = 0;
