@@ -247,7 +247,8 @@ __host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, in
     l.hp = o;   o = up(o + 4 * 2 * P);
     o = o > pl_end ? o : pl_end;
     l.coef = o; o = up(o + coef_bytes);
-    l.red = o;  o = up(o + 8 * nw * (nsum > 16 ? nsum : 16));
+    /* the int8-MFMA path's pruning tiers alternate between two copies (one barrier per test) */
+    l.red = o;  o = up(o + 8 * nw * (nsum > 16 ? nsum : 16) * (planes ? 2 : 1));
     l.dec = o;  o = up(o + (int)sizeof(Decision));
     l.rb = o;   o = up(o + 8 * 32);
     l.misc = o; o = up(o + 4 * 8);

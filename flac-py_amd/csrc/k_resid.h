@@ -783,19 +783,19 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
         }
     };
     /* this wave's running LPC sums (cumulative over tiers) into red */
-    auto store = [&]() __attribute__((always_inline)) {
+    auto store = [&](unsigned long long* buf) __attribute__((always_inline)) {
 #pragma unroll
         for (int nt = 0; nt < NTMAX; ++nt) {
             uint64_t v = acc[nt];
             v += (uint64_t)__shfl_xor((unsigned long long)v, 16);
             v += (uint64_t)__shfl_xor((unsigned long long)v, 32);
             const int p = 16 * nt + col + 1;
-            if (lane < 16 && p <= LMAX) red[wid * NSUM + 4 + p] = p <= L ? v : 0ull;
+            if (lane < 16 && p <= LMAX) buf[wid * NSUM + 4 + p] = p <= L ? v : 0ull;
         }
     };
     if (!prune) {
         go(wid, nw);
-        store();
+        store(red);
         return 0;
     }
     /* ablation (timing only, FLACMI_DEBUG_STOP): 13 fixed sums alone, 14 the first quarter of
@@ -804,11 +804,17 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
     if (dbg == 13) return 0x100;
     if (dbg == 14 || dbg == 15) {
         go(wid, dbg == 14 ? 4 * nw : nw);
-        store();
+        store(red);
         return 0x100 | (dbg == 14 ? 2 : 8);
     }
     bool pruned = false;
     int done = 0;
+    uint64_t fmin = ~0ull; /* the best exact fixed sum (read at the first test) */
+    /* tier t stores its running sums into red when 7 - t is even (the last tier's exact sums
+     * land where phase D reads them), else into the copy after it: a wave that starts the
+     * next tier stores while slower waves may still read this one's, so a test needs one
+     * barrier, not two */
+    unsigned long long* const red_alt = red + nw * NSUM;
     /* eighths of the wave's tiles, spread over the block (residues 0, 4, 2, 6, 1, 5, 3, 7 of
      * the wave's tile index mod 8): a unit stops at the first eighth whose partial LPC sums
      * all exceed the best fixed sum (config 3: LPC sums run ~4x the fixed ones, so most
@@ -824,22 +830,26 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
         } else {
             go(wid + res * nw, kTiers * nw);
         }
-        store();
+        unsigned long long* const buf = ((kTiers - 1 - t) & 1) ? red_alt : red;
+        store(buf);
         done = t + 1;
         if (t == kTiers - 1) break; /* every tile done: the sums are exact */
         __syncthreads();
-        uint64_t tj = 0;
-        if (lane < NSUM)
-            for (int w2 = 0; w2 < nw; ++w2) tj += red[w2 * NSUM + lane];
-        uint64_t fmin = ~0ull;
+        if (fmin == ~0ull) { /* first test: the fixed sums (exact, stored before the tiers) */
+            uint64_t tf = 0;
+            if (lane < 5)
+                for (int w2 = 0; w2 < nw; ++w2) tf += red[w2 * NSUM + lane];
 #pragma unroll
-        for (int o = 0; o < 5; ++o) {
-            const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tj >> 32), o) << 32) |
-                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tj, o);
-            fmin = v < fmin ? v : fmin;
+            for (int o = 0; o < 5; ++o) {
+                const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tf >> 32), o) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tf, o);
+                fmin = v < fmin ? v : fmin;
+            }
         }
+        uint64_t tj = 0;
+        if (lane >= 5 && lane < 5 + L)
+            for (int w2 = 0; w2 < nw; ++w2) tj += buf[w2 * NSUM + lane];
         pruned = __ballot(lane >= 5 && lane < 5 + L && tj <= fmin) == 0;
-        __syncthreads(); /* every wave has read red before the next tier stores */
         if (pruned) break;
     }
     return done | (pruned ? 0x100 : 0);
