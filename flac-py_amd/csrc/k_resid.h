@@ -1291,8 +1291,7 @@ next_unit:
                  * whether every top digit fits a signed byte */
                 uint32_t* pw = reinterpret_cast<uint32_t*>(smem + lay.pl);
                 const int pwd = PLB >> 2;
-                uint32_t xm = 0;
-                bool b2ok = true;
+                int32_t xhi = 0, xlo = 0; /* the thread's largest and smallest samples (0: neutral) */
                 /* eight 16-byte loads in flight per thread before any is used (clamped
                  * indices, no guarded loads) */
                 constexpr int KB = 8;
@@ -1309,21 +1308,24 @@ next_unit:
                         if (v >= nv) break;
                         const int4v q = qv[k];
                         *reinterpret_cast<int4v*>(xs32 + 4 * v) = q;
-                        uint32_t w0 = 0, w1 = 0, w2 = 0;
+                        /* balanced digits (mf8_digits) by bytes: x + 0x808080 has the unsigned
+                         * digits d + 128 of x's balanced ones, so its bytes XOR 0x80 are the
+                         * int8 digits b0, b1, b2 (valid while -0x808080 <= x <= 0x7f7f7f) */
+                        uint32_t t[4];
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
-                            int32_t b0, b1, b2;
-                            mf8_digits(q[e], b0, b1, b2);
-                            b2ok &= b2 <= 127;
-                            const uint32_t ax = (uint32_t)(q[e] < 0 ? -q[e] : q[e]);
-                            xm = ax > xm ? ax : xm;
-                            w0 |= ((uint32_t)b0 & 255u) << (8 * e);
-                            w1 |= ((uint32_t)b1 & 255u) << (8 * e);
-                            w2 |= ((uint32_t)b2 & 255u) << (8 * e);
+                            t[e] = ((uint32_t)q[e] + 0x808080u) ^ 0x808080u;
+                            xhi = q[e] > xhi ? q[e] : xhi;
+                            xlo = q[e] < xlo ? q[e] : xlo;
                         }
-                        pw[(kMf8Pad >> 2) + v] = w0;
-                        pw[pwd + (kMf8Pad >> 2) + v] = w1;
-                        pw[2 * pwd + (kMf8Pad >> 2) + v] = w2;
+                        /* (b0 t0, b0 t1, b1 t0, b1 t1) and the same for t2, t3, then the planes */
+                        const uint32_t p01 = __builtin_amdgcn_perm(t[1], t[0], 0x05010400u);
+                        const uint32_t p23 = __builtin_amdgcn_perm(t[3], t[2], 0x05010400u);
+                        const uint32_t q01 = __builtin_amdgcn_perm(t[1], t[0], 0x0c0c0602u);
+                        const uint32_t q23 = __builtin_amdgcn_perm(t[3], t[2], 0x0c0c0602u);
+                        pw[(kMf8Pad >> 2) + v] = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+                        pw[pwd + (kMf8Pad >> 2) + v] = __builtin_amdgcn_perm(p23, p01, 0x07060302u);
+                        pw[2 * pwd + (kMf8Pad >> 2) + v] = __builtin_amdgcn_perm(q23, q01, 0x05040100u);
                     }
                 }
                 /* zero pads: the first kMf8Pad bytes and the tail of each plane (only those
@@ -1333,6 +1335,10 @@ next_unit:
                     const int pl = i / npad, k = i - pl * npad;
                     pw[pl * pwd + (k < head ? k : tail0 + (k - head))] = 0u;
                 }
+                /* every top digit an int8 (both ends: 25-bit and wider samples reach below
+                 * -0x808080), else the int64 chains */
+                const bool b2ok = xhi <= 0x7f7f7f && xlo >= -0x808080;
+                const uint32_t xm = max((uint32_t)xhi, 0u - (uint32_t)xlo);
                 uint32_t wm = b2ok ? xm : 0xffffffffu;
 #pragma unroll
                 for (int o = 32; o >= 1; o >>= 1) {

@@ -285,7 +285,8 @@ def test_int8_mfma_candidate_sums_orders(az, L, bits):
 
 def test_int8_mfma_fallbacks(az):
     """Units the int8 path must hand to the int64 chains: a top digit of 128 (a sample above
-    8355711), n not a multiple of 16; next to ordinary units and the most negative sample."""
+    8355711) or of -129 (a 25-bit sample below -8421504), n not a multiple of 16; next to
+    ordinary units, the most negative 24-bit sample and both ends of the int8 digit range."""
     n = 2048
     a = oracle.synth_batch(0, 12, n, 24, 77, dtype=np.int32)
     a[1, 700] = 8355712
@@ -295,6 +296,17 @@ def test_int8_mfma_fallbacks(az):
     out = az.analyze(a, make_params(32, 15, 0, 6), n, sample_bits=24, debug=True)
     ora = oracle.analyze_batch(a, oracle.make_params(32, 15, 0, 6), n, sample_bits=24, threads=16)
     compare_with_oracle(out, ora, [n] * len(a))
+    # 25-bit samples: the top digit leaves int8 below -0x808080 as well as above 0x7f7f7f
+    c = oracle.synth_batch(100, 8, n, 25, 78, dtype=np.int32) // 4
+    c[1, 300] = -0x808081  # one past the lower end: the int64 chains
+    c[2, 301] = -0x808080  # the lower end itself: still int8 digits
+    c[3, 302] = 0x7f7f7f
+    c[4, 303:310] = -0x900000
+    for bits in (25, 24):
+        cc = c if bits == 25 else np.clip(c, -2 ** 23, 2 ** 23 - 1)
+        out = az.analyze(cc, make_params(32, 15, 0, 6), n, sample_bits=bits, debug=True)
+        ora = oracle.analyze_batch(cc, oracle.make_params(32, 15, 0, 6), n, sample_bits=bits, threads=16)
+        compare_with_oracle(out, ora, [n] * len(cc))
     m = 2040  # n % 16 != 0
     b = np.ascontiguousarray(a[:, :m])
     out = az.analyze(b, make_params(32, 15, 0, 3), m, sample_bits=24, debug=True)
