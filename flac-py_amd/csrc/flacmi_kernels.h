@@ -59,6 +59,8 @@ struct ResidArgs {
     int32_t prune;                   /* 1 = reference mode may skip the exact LPC candidate sums of a unit
                                         whose lower bounds already lose to the best fixed sum
                                         (meta lpc_order = lpc_sum = FLACMI_LPC_PRUNED) */
+    int32_t persist;                 /* k_resid kVarMf8: the grid loops over the batch and copies the next
+                                        unit's samples into LDS (LDS-DMA) during this unit's Rice phase */
 };
 /* internal unit status between the fast and the generic k_resid (never returned) */
 #define FLACMI_STATUS_RETRY 0x7e

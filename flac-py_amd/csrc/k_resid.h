@@ -1056,17 +1056,29 @@ __device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta
  *                *retry_count, every path. */
 enum { kVarGeneric = 0, kVarFast = 1, kVarList = 2, kVarMf8 = 3, kVarList1 = 4 };
 /* kVarMf8 (PATH_W64, LMAX >= 16): only the int8-MFMA path, fixed-predictor choice and the
- * wide Rice step, in 1024-thread workgroups (four waves per SIMD instead of two: the unit's
- * 140 KB of LDS allows one workgroup per CU either way); a unit that needs anything else
+ * wide Rice step, as a persistent grid (a.persist: one workgroup per CU loops over the batch;
+ * the unit's 140 KB of LDS allows one workgroup per CU anyway) that copies the next unit's
+ * samples into LDS during this unit's Rice phase; a unit that needs anything else
  * (outside the int8 bounds, an LPC or order > 4 choice, another Rice shape) is marked
  * FLACMI_STATUS_RETRY and listed for kVarList1: the 512-thread generic body, one workgroup
  * per unit of the batch, retry_list[blockIdx.x] below *retry_count (no unit loop: the
  * looping list variant of the 64-bit path spills) */
 __host__ __device__ constexpr int resid_launch_bound(int path, int lmax, int var) {
-    return var == kVarMf8 ? 1024 : path >= PATH_W64 ? 512 : 256;
+    return path >= PATH_W64 ? 512 : 256;
 }
+/* the kernel's argument block (k_resid's only argument, at offset 0 of the kernarg segment)
+ * through a pointer the compiler cannot follow across the persistent variant's unit loop
+ * (else it keeps every field live in registers across it); the kernarg pointer itself, not
+ * the address of the parameter, which would copy it to scratch */
+typedef const __attribute__((address_space(4))) ResidArgs* KernargArgs;
+__device__ __forceinline__ KernargArgs opaque_args() {
+    KernargArgs p = (KernargArgs)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
 template <int LMAX, int PATH, typename ResT, int VAR>
-__global__ __launch_bounds__(resid_launch_bound(PATH, LMAX, VAR)) void k_resid(ResidArgs a) {
+__global__ __launch_bounds__(resid_launch_bound(PATH, LMAX, VAR)) void k_resid(ResidArgs a_in) {
     constexpr bool FAST = VAR == kVarFast;
     constexpr bool M8V = VAR == kVarMf8;
     static_assert(!M8V || (PATH == PATH_W64 && LMAX >= 16 && sizeof(ResT) == 4), "kVarMf8: int8-MFMA units only");
@@ -1076,10 +1088,20 @@ __global__ __launch_bounds__(resid_launch_bound(PATH, LMAX, VAR)) void k_resid(R
      * workgroup-uniform, so each one goes to the next listed unit. */
     int64_t li = blockIdx.x, gid = blockIdx.x;
     if constexpr (VAR == kVarList || VAR == kVarList1) {
-        if (li >= (int64_t)*a.retry_count) return;
+        if (li >= (int64_t)*a_in.retry_count) return;
     }
+    /* kVarMf8 persistent: this unit's samples already sit in LDS (copied during the previous
+     * unit's Rice phase) */
+    bool pre = false;
 next_unit:
+    auto&& a = [&]() -> decltype(auto) {
+        if constexpr (VAR == kVarMf8) return *opaque_args();
+        else return (a_in);
+    }();
     if constexpr (VAR == kVarList || VAR == kVarList1) gid = a.retry_list[li];
+    if constexpr (VAR == kVarMf8) gid = li;
+    const bool pre_now = pre; /* consumed by this unit's staging */
+    pre = false;
     {
     using UX = ResT;
     constexpr bool S16 = PATH == PATH_S16;
@@ -1295,19 +1317,24 @@ next_unit:
                 /* eight 16-byte loads in flight per thread before any is used (clamped
                  * indices, no guarded loads) */
                 constexpr int KB = 8;
+                if (M8V && pre_now) { /* every wave's copies of this unit have landed */
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                }
                 for (int v0 = tid; v0 < nv; v0 += KB * NT) {
                     int4v qv[KB];
 #pragma unroll
                     for (int k = 0; k < KB; ++k) {
                         const int v = v0 + k * NT < nv ? v0 + k * NT : nv - 1;
-                        qv[k] = *reinterpret_cast<const int4v*>(src + 4 * v);
+                        qv[k] = (M8V && pre_now) ? *reinterpret_cast<const int4v*>(xs32 + 4 * v)
+                                                 : *reinterpret_cast<const int4v*>(src + 4 * v);
                     }
 #pragma unroll
                     for (int k = 0; k < KB; ++k) {
                         const int v = v0 + k * NT;
                         if (v >= nv) break;
                         const int4v q = qv[k];
-                        *reinterpret_cast<int4v*>(xs32 + 4 * v) = q;
+                        if (!(M8V && pre_now)) *reinterpret_cast<int4v*>(xs32 + 4 * v) = q;
                         /* balanced digits (mf8_digits) by bytes: x + 0x808080 has the unsigned
                          * digits d + 128 of x's balanced ones, so its bytes XOR 0x80 are the
                          * int8 digits b0, b1, b2 (valid while -0x808080 <= x <= 0x7f7f7f) */
@@ -1518,7 +1545,7 @@ next_unit:
     } else if (MF8 && use_mf8) {
         if constexpr (MF8)
         {
-            const int r = mf8_candidate_sums<LMAX, !M8V>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
+            const int r = mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
                                                    nw, red, a.prune != 0 && !lpc_only && !rice_only, a.stop_after);
             lpc_pruned = (r >> 8) != 0;
             lpc_tiers = r ? (r & 0xff) | (8 << 8) : 0;
@@ -1976,6 +2003,28 @@ next_unit:
     }
     if constexpr (WIDE && sizeof(ResT) == 4) {
         if (wr_om >= 0) {
+            /* kVarMf8 persistent: copy the next unit's samples into the staging region (dead
+             * since the chosen-residual pass) while the Rice phase runs; the barriers up to
+             * the next unit are raw (lgkmcnt only), or their vmcnt(0) would drain the copies */
+            if constexpr (M8V) {
+                const int64_t nx = li + gridDim.x;
+                pre = a.persist && nx < a.count && (n & 255) == 0;
+                if (pre) {
+                    const int32_t* __restrict__ nsrc = (const int32_t*)a.samples + (a.unit0 + nx) * a.stride;
+                    for (int b = wid; b < (n >> 8); b += nw) /* 1 KB (256 samples) per wave-instruction */
+                        __builtin_amdgcn_global_load_lds((const void*)(nsrc + 256 * b + 4 * lane),
+                                                         (void __attribute__((address_space(3)))*)(xs32 + 256 * b), 16, 0, 0);
+                }
+            }
+            auto rbar = [&]() __attribute__((always_inline)) {
+                if constexpr (M8V) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_s_barrier();
+                    asm volatile("" ::: "memory");
+                } else {
+                    __syncthreads();
+                }
+            };
             /* Every heap node's parameter at once (encoder.py:655-760), one node per thread:
              *  1. wave 0: prefix sums of the finest sums (hs[P..2P), left by phase E) into the
              *     generic path's heap-parameter region (unused here): pre(k), k = 1..P;
@@ -2012,7 +2061,7 @@ next_unit:
                 if (lane < 16) rb[lane] = 0;
                 if (lane == 0) misc[0] = 0x7fffffff, misc[4] = 0;
             }
-            __syncthreads();
+            rbar();
             {
                 const bool intlog = n <= 16384; /* S < n 2^32 <= 2^46: exact integer floor(log2(S / len)) */
                 for (int j0 = (1 << ro); j0 < 2 * P; j0 += NT) {
@@ -2054,7 +2103,7 @@ next_unit:
                     }
                 }
             }
-            __syncthreads();
+            rbar();
             if (a.stop_after == 5) goto unit_done; /* ablation: after the parameters */
             if (misc[0] != 0x7fffffff) {
                 if (tid == 0)
@@ -2084,7 +2133,7 @@ next_unit:
                 w[3] |= ((dmax >= 16 ? 1u : 0u) << 16) | (pm << 24);
                 *reinterpret_cast<uint4*>(pk + 16 * k) = uint4{w[0], w[1], w[2], w[3]};
             }
-            __syncthreads();
+            rbar();
             if (a.stop_after == 6) goto unit_done; /* ablation: after the row transform */
             const uint4* pkv = reinterpret_cast<const uint4*>(hs);
             uint64_t tb[16];
@@ -2163,7 +2212,7 @@ next_unit:
                         }
                 }
             }
-            __syncthreads();
+            rbar();
             if (wid == 0) {
                 /* lane o: order o's total (its nw partials loaded side by side, not one thread
                  * walking every order and wave); the first minimum (encoder.py:740-760) by
@@ -2336,6 +2385,18 @@ next_unit:
     } /* !FAST */
     }
 unit_done:
+    if constexpr (M8V) {
+        if (a.persist) {
+            li += gridDim.x;
+            if (li < a.count) {
+                /* every wave is done with this unit's LDS (raw: the copies stay in flight) */
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                goto next_unit;
+            }
+        }
+    }
     if constexpr (VAR == kVarList) {
         li += gridDim.x;
         if (li < (int64_t)*a.retry_count) {
@@ -2423,23 +2484,30 @@ static inline bool resid_fast_ok(const ResidArgs& a) {
 }
 
 /* FLACMI_MF8_1024=1: config-3 shapes through kVarMf8 (opt-in while it is measured) */
-static inline bool mf8_1024_enabled() {
+static inline bool mf8_persist_enabled() {
     static const bool on = [] {
-        const char* e = getenv("FLACMI_MF8_1024");
+        const char* e = getenv("FLACMI_MF8_PERSIST");
         return e && e[0] == '1';
     }();
     return on;
 }
 
-/* kVarMf8 over the batch (1024 threads per unit), then the 512-thread list variant over the
- * units it listed */
+/* kVarMf8 as a persistent grid (one workgroup per CU), then the list variant over the units
+ * it listed */
 template <int LMAX>
-static hipError_t launch_resid_mf8(const ResidArgs& a, hipStream_t s) {
+static hipError_t launch_resid_mf8(const ResidArgs& a_in, hipStream_t s) {
+    ResidArgs a = a_in;
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
     const int P = 1 << (rmax_eff < 0 ? 0 : rmax_eff);
-    const int nt8 = 1024, ntl = resid_threads(a.n, true);
+    const int nt8 = resid_threads(a.n, true), ntl = nt8;
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+        ncu = 256;
+    a.persist = 1;
+    const int64_t grid = a.count < ncu ? a.count : ncu;
     const size_t lds8 = resid_lds_layout(LMAX, a.n, nt8 / 64, P, 4, 4, CoefTables<LMAX>::BYTES, false, true).total;
     const size_t ldsl = resid_lds_layout(LMAX, a.n, ntl / 64, P, 4, 4, CoefTables<LMAX>::BYTES, false, true).total;
     hipError_t e = hipMemsetAsync(a.retry_count, 0, sizeof(unsigned long long), s);
@@ -2447,7 +2515,7 @@ static hipError_t launch_resid_mf8(const ResidArgs& a, hipStream_t s) {
     auto k8 = k_resid<LMAX, PATH_W64, uint32_t, kVarMf8>;
     if ((e = hipFuncSetAttribute((const void*)k8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds8)) != hipSuccess)
         return e;
-    hipLaunchKernelGGL(k8, dim3((unsigned)a.count), dim3(nt8), lds8, s, a);
+    hipLaunchKernelGGL(k8, dim3((unsigned)grid), dim3(nt8), lds8, s, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_poison_lds(s)) != hipSuccess) return e;
     auto kl = k_resid<LMAX, PATH_W64, uint32_t, kVarList1>;
@@ -2462,7 +2530,7 @@ static hipError_t launch_resid_bucket(const ResidArgs& a, int path, int rb, hipS
     if (rb == 8) return launch_resid_T<LMAX, PATH_W64, uint64_t>(a, s);
     if constexpr (LMAX >= 16)
         if (path == PATH_W64 && a.mode == FLACMI_MODE_REFERENCE && a.mfma && a.retry_list && a.retry_count &&
-            a.sample_bytes == 4 && a.L >= 1 && a.n % 16 == 0 && a.n >= 8192 && mf8_1024_enabled())
+            a.sample_bytes == 4 && a.L >= 1 && a.n % 256 == 0 && a.n >= 8192 && mf8_persist_enabled())
             return launch_resid_mf8<LMAX>(a, s);
     if constexpr (LMAX == 8 || LMAX == 12)
         if (path == PATH_S16 && resid_fast_ok(a)) return launch_resid_fast<LMAX>(a, s);

@@ -601,11 +601,7 @@ def test_production_batches_vs_oracle(az, cfg):
 # mf8_candidate_sums) against the oracle, with the tier that decided each unit
 # ---------------------------------------------------------------------------------------
 def _resid_threads_wide(n):
-    """device_common.h resid_threads(n, wide=true): k_resid's workgroup on the 64-bit paths
-    (1024 threads: k_resid.h kVarMf8, which FLACMI_MF8_1024=1 selects for n >= 8192)."""
-    import os
-    if os.environ.get("FLACMI_MF8_1024") == "1" and n >= 8192 and n % 16 == 0:
-        return 1024
+    """device_common.h resid_threads(n, wide=true): k_resid's workgroup on the 64-bit paths."""
     nch = (n + 7) // 8
     nt = 64 * ((nch + 64 * 3 - 1) // (64 * 3))
     return max(64, min(nt, 512))
