@@ -66,8 +66,11 @@ __device__ __forceinline__ void lpc_finish(const double (&acc)[LMAX + 1], const 
 #pragma unroll
                 for (int j = 2; j <= LMAX; ++j)
                     if (j <= p && __builtin_fabs(c[j]) > cm) cm = __builtin_fabs(c[j]);
-                int32_t qv[LMAX];
-                int nq = 0, shift = 0;
+                /* the quantised coefficients go straight into the record (no qv[LMAX] array held
+                 * beside c[] and acc[]: 32 VGPRs at L = 32); an order that fails leaves the
+                 * record's status set, so what it wrote is never read */
+                int32_t* __restrict__ cq = rec + 2 + L + (p * (p - 1)) / 2;
+                int shift = 0;
                 if (!(cm > 0.0)) {
                     qst = ST_ASSERT;
                     qsite = FLACMI_SITE_QUANT_CMAX;
@@ -98,19 +101,19 @@ __device__ __forceinline__ void lpc_finish(const double (&acc)[LMAX + 1], const 
                                     const double r = __builtin_rint(e);
                                     const double qq = r < qmin ? qmin : (r > qmax ? qmax : r);
                                     e = e - qq;
-                                    qv[j - 1] = (int32_t)qq;
+                                    cq[j - 1] = (int32_t)qq;
                                 }
                             }
                         }
                         if (qst == ST_OK) {
-                            if (neg) {
+                            if (neg) { /* ([], 0) (encoder.py:523-532): no coefficients, shift 0 */
                                 negmask |= 1u << k;
                                 shift = 0;
-                                nq = 0;
-                            } else {
-                                nq = p;
+#pragma unroll
+                                for (int j = 0; j < LMAX; ++j)
+                                    if (j < p) cq[j] = 0;
                             }
-                            write_quant<LMAX>(rec, L, p, qv, nq, shift);
+                            rec[2 + p - 1] = shift;
                         }
                     }
                 }

@@ -530,9 +530,11 @@ __device__ __forceinline__ void mf8_digits(int32_t x, int32_t& b0, int32_t& b1, 
 }
 
 /* a 16-byte window of a plane at any byte alignment (tile T of the lane's window starts 16 T
- * bytes after p): one unaligned ds_read_b128 (gfx950 reads LDS at any byte address), or with
- * -DFLACMI_MF8_ALIGNBYTE the five dwords that cover it and four v_alignbyte by its offset */
-#ifndef FLACMI_MF8_ALIGNBYTE
+ * bytes after p): the five dwords that cover it and four v_alignbyte by its offset.  With
+ * -DFLACMI_MF8_UNALIGNED one unaligned ds_read_b128 instead (gfx950 accepts it, but measured
+ * c3 k_resid 55.1 against 39.4 ms: an unaligned 16-byte LDS read is far slower than the five
+ * aligned dword reads and four v_alignbyte, profiles/r04c) */
+#ifdef FLACMI_MF8_UNALIGNED
 struct Mf8Raw {
     v4i v;
 };
