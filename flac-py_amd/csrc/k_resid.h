@@ -2486,10 +2486,11 @@ static inline bool resid_fast_ok(const ResidArgs& a) {
 }
 
 /* FLACMI_MF8_1024=1: config-3 shapes through kVarMf8 (opt-in while it is measured) */
+/* FLACMI_MF8_PERSIST=0: config-3 shapes through the generic k_resid launch instead */
 static inline bool mf8_persist_enabled() {
     static const bool on = [] {
         const char* e = getenv("FLACMI_MF8_PERSIST");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     return on;
 }
@@ -2503,7 +2504,7 @@ static hipError_t launch_resid_mf8(const ResidArgs& a_in, hipStream_t s) {
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
     const int P = 1 << (rmax_eff < 0 ? 0 : rmax_eff);
-    const int nt8 = resid_threads(a.n, true), ntl = nt8;
+    const int nt8 = resid_threads(a.n, true), ntl = nt8; /* 512 */
     int dev = 0, ncu = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         ncu <= 0)
