@@ -2485,7 +2485,6 @@ static inline bool resid_fast_ok(const ResidArgs& a) {
            resid_regz(a.n, rmax_eff, true) && (a.n + 7) / 8 + 1 >= a.rec_words;
 }
 
-/* FLACMI_MF8_1024=1: config-3 shapes through kVarMf8 (opt-in while it is measured) */
 /* FLACMI_MF8_PERSIST=0: config-3 shapes through the generic k_resid launch instead */
 static inline bool mf8_persist_enabled() {
     static const bool on = [] {
