@@ -2012,10 +2012,18 @@ next_unit:
                 const int64_t nx = li + gridDim.x;
                 pre = a.persist && nx < a.count && (n & 255) == 0;
                 if (pre) {
+                    /* in inline asm: issued through the builtin, the LDS-DMA makes the compiler
+                     * wait for it (vmcnt(0)) before the Rice phase's next LDS access, whatever
+                     * address that touches, which drains the copy at once.  This region is not
+                     * read before the next unit's staging, which waits for it explicitly. */
                     const int32_t* __restrict__ nsrc = (const int32_t*)a.samples + (a.unit0 + nx) * a.stride;
+                    const uint32_t lbase = (uint32_t)reinterpret_cast<uintptr_t>(
+                        (const __attribute__((address_space(3))) int32_t*)xs32);
                     for (int b = wid; b < (n >> 8); b += nw) /* 1 KB (256 samples) per wave-instruction */
-                        __builtin_amdgcn_global_load_lds((const void*)(nsrc + 256 * b + 4 * lane),
-                                                         (void __attribute__((address_space(3)))*)(xs32 + 256 * b), 16, 0, 0);
+                        asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off"
+                                     :
+                                     : "s"(lbase + 1024u * (uint32_t)b), "v"(nsrc + 256 * b + 4 * lane)
+                                     : "memory", "m0");
                 }
             }
             auto rbar = [&]() __attribute__((always_inline)) {
