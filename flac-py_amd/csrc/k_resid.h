@@ -1095,6 +1095,7 @@ __global__ __launch_bounds__(resid_launch_bound(PATH, LMAX, VAR)) void k_resid(R
     /* kVarMf8 persistent: this unit's samples already sit in LDS (copied during the previous
      * unit's Rice phase) */
     bool pre = false;
+    int32_t pre_st = 0, pre_rv0 = 0, pre_rv1 = 0; /* ... and its record's status and words tid, tid + NT */
 next_unit:
     auto&& a = [&]() -> decltype(auto) {
         if constexpr (VAR == kVarMf8) return *opaque_args();
@@ -1256,14 +1257,17 @@ next_unit:
 
     /* the unit's LPC status: loaded now, tested after the staging loads are in flight (a
      * test here would put one more HBM round trip in front of them) */
-    const int st_rec = ref_mode ? rec[0] : 0;
+    const int st_rec = (M8V && pre_now) ? pre_st : ref_mode ? rec[0] : 0;
     /* int8-MFMA builds: the record's words tid and tid + NT, loaded beside the samples (the
      * coefficient table is scattered from them after the staging loop instead of gathered
      * from HBM in a second round trip); clamped indices, no guarded loads */
     int32_t rv[2] = {0, 0};
     const bool rec_regs = MF8 && do_lpc && 2 * NT >= a.rec_words;
     if constexpr (MF8) {
-        if (rec_regs) {
+        if (M8V && pre_now) {
+            rv[0] = pre_rv0;
+            rv[1] = pre_rv1;
+        } else if (rec_regs) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) rv[j] = rec[min(tid + j * NT, a.rec_words - 1)];
         }
@@ -2010,8 +2014,14 @@ next_unit:
              * the next unit are raw (lgkmcnt only), or their vmcnt(0) would drain the copies */
             if constexpr (M8V) {
                 const int64_t nx = li + gridDim.x;
-                pre = a.persist && nx < a.count && (n & 255) == 0;
+                pre = a.persist && nx < a.count && (n & 255) == 0 && 2 * NT >= a.rec_words;
                 if (pre) {
+                    /* the next unit's record status and words (registers: 3 VGPRs across the
+                     * unit boundary) */
+                    const int32_t* __restrict__ nrec = a.rec + nx * a.rec_words;
+                    pre_st = nrec[0];
+                    pre_rv0 = nrec[min(tid, a.rec_words - 1)];
+                    pre_rv1 = nrec[min(tid + NT, a.rec_words - 1)];
                     /* in inline asm: issued through the builtin, the LDS-DMA makes the compiler
                      * wait for it (vmcnt(0)) before the Rice phase's next LDS access, whatever
                      * address that touches, which drains the copy at once.  This region is not
@@ -2223,10 +2233,11 @@ next_unit:
                 }
             }
             rbar();
-            if (wid == 0) {
-                /* lane o: order o's total (its nw partials loaded side by side, not one thread
-                 * walking every order and wave); the first minimum (encoder.py:740-760) by
-                 * key = total * 16 + order over lanes 0..15 */
+            {
+                /* every wave: lane o holds order o's total (its nw partials loaded side by side);
+                 * the first minimum (encoder.py:740-760) by key = total * 16 + order over lanes
+                 * 0..15.  Wave 0 writes the meta record; every thread one Rice parameter (was
+                 * wave 0 alone, four per lane, with the workgroup's LDS held meanwhile). */
                 const bool cand = lane >= ro && lane <= oo;
                 unsigned long long v = 0;
                 if (cand) {
@@ -2243,10 +2254,11 @@ next_unit:
                 const unsigned long long bits = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane(
                                                      (int)(uint32_t)(key >> 36)) << 32) |
                                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(key >> 4));
-                put_meta_wave(meta, lane, ST_OK, 0, dec, start, n - start, best, 1 << best,
-                              ((misc[4] >> best) & 1) ? 5 : 4, (long long)bits);
+                if (wid == 0)
+                    put_meta_wave(meta, lane, ST_OK, 0, dec, start, n - start, best, 1 << best,
+                                  ((misc[4] >> best) & 1) ? 5 : 4, (long long)bits);
                 int32_t* __restrict__ rp = a.rice_params + gid * a.params_stride;
-                for (int K = lane; K < (1 << best); K += 64) {
+                for (int K = tid; K < (1 << best); K += NT) {
                     const int row = 16 * (K << (omax - best));
                     rp[K] = pk[row + 15] + pk[row + best]; /* pm + delta */
                 }
