@@ -73,6 +73,7 @@ struct SLds {
  *   red  u64 [nw][group][order] MFMA partial sums               MFMA phase .. choice
  *   red2 u64 [nw + 1][order] data bits (aliases red)            Rice (after B3)
  *   red0 u32 [nw] sum|x|                                         staging .. choice
+ *        (word 0 then: the Rice table's error flag                 B3 .. B3b)
  *   pks  u32 [P] finest partition sums                          staging (zeroed) .. Rice */
 __host__ __device__ inline SLds stream_lds(int n, int nw, int tap_words, int P, int RS) {
     auto up = [](int b) { return (b + 15) & ~15; };
@@ -349,6 +350,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             const int32_t* r = a.rec + gid * a.rec_words;
 #pragma unroll
             for (int j = 0; j < kTJ; ++j) {
+                if (j > 0 && j * NT >= kTW) break; /* uniform: a two-wave unit needs j = 0 only */
                 const int gw = tid + j * NT, p = gw / 10 + 1, w = gw - 10 * (p - 1);
                 const int pc = p < L ? p : L, base = 2 + L + (pc * (pc - 1)) / 2;
                 /* T_p[16 - 2w] (the shift for w = 8: T_p[0] = -2^shift) and T_p[15 - 2w] */
@@ -378,6 +380,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             uint32_t* tt = reinterpret_cast<uint32_t*>(recl);
 #pragma unroll
             for (int j = 0; j < kTJ; ++j) {
+                if (j > 0 && j * NT >= kTW) break;
                 const int gw = tid + j * NT, p = gw / 10 + 1, w = gw - 10 * (p - 1);
                 if (gw < kTW) {
                     auto tap = [&](int i, int32_t c) -> uint32_t {
@@ -800,64 +803,67 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         return;
     }
     const int ro = R05 ? 0 : __builtin_amdgcn_readfirstlane(a.rmin), oo = R05 ? 5 : __builtin_amdgcn_readfirstlane(omax);
-    /* every wave, lane j - 1 = heap node j = (order o, partition K), j = 2^o + K < 2P <= 64:
+    /* wave 0 only (the other waves wait at the barrier below, their SIMD slots going to other
+     * workgroups): lane j - 1 = heap node j = (order o, partition K), j = 2^o + K < 2P <= 64:
      * node sums from a prefix over the finest sums, one parameter each, the first error in
      * the reference's evaluation order = the lowest node (orders ascending, then partitions) */
     /* 32 bits: the chosen predictor's sum|r| is at most the order-0 sum n * 2^15, so its
      * zig-zag total stays below 2 * 10240 * 2^15 + n < 2^32 */
-    uint32_t pre = lane < P ? pks[lane] : 0u;
-#pragma unroll
-    for (int d = 1; d < 32; d <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)pre, (unsigned)d);
-        if (lane >= d) pre += t;
-    }
     const int j = lane + 1;
     const int o = 31 - __builtin_clz((unsigned)j);
     const int K = j - (1 << o), dd = oo - o;
     const bool valid = j < 2 * P && o >= ro;
-    const int hi_k = ((K + 1) << (dd < 0 ? 0 : dd)) - 1, lo_k = (K << (dd < 0 ? 0 : dd)) - 1;
-    const uint32_t ph = (uint32_t)__shfl((int)pre, hi_k & 63);
-    const uint32_t pl = (uint32_t)__shfl((int)pre, lo_k & 63);
-    const uint32_t snode = ph - (lo_k >= 0 ? pl : 0u);
     const int len = (n >> (o < 16 ? o : 15)) - (K == 0 ? order : 0);
-    const bool zero = snode == 0;
-    const int prm = (zero || !valid) ? 0 : rice_param_exact((uint64_t)snode, len);
-    {
-        const unsigned long long eb = __ballot(valid && (zero || prm < 0));
-        if (eb) {
-            if (wid == 0) {
-                const int kl = __builtin_ctzll(eb);
-                mv.status = ST_VALUE;
-                mv.site = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
-                store_meta(meta, lane, mv, coefl);
-            }
-            return;
-        }
-    }
-    /* this wave's table: finest partition k (lane k) -> the parameter of its ancestor at
-     * every order, as p | p << 16 */
-    int pmax = 0;
-    /* (opaque: lane * 16 bytes would otherwise be shared with the staging's kFixB offset and
-     * held, or spilled, across the whole kernel) */
-    uint16_t* const prow = pkw + (int)opaque((uint32_t)lane) * RS;
+    int prm = 0;
+    uint32_t* const eflag = red0; /* free after B2's reads */
+    if (wid == 0) {
+        uint32_t pre = lane < P ? pks[lane] : 0u;
 #pragma unroll
-    for (int o2 = 0; o2 < kRiceOrders; ++o2) {
-        if (o2 >= ro && o2 <= oo) {
-            const int node = (1 << o2) + (lane >> (oo - o2));
-            const int pv = __shfl(prm, (node - 1) & 63);
-            pmax = max(pmax, pv);
-            if (lane < P) prow[o2] = (uint16_t)pv;
+        for (int d = 1; d < 32; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)pre, (unsigned)d);
+            if (lane >= d) pre += t;
+        }
+        const int hi_k = ((K + 1) << (dd < 0 ? 0 : dd)) - 1, lo_k = (K << (dd < 0 ? 0 : dd)) - 1;
+        const uint32_t ph = (uint32_t)__shfl((int)pre, hi_k & 63);
+        const uint32_t pl = (uint32_t)__shfl((int)pre, lo_k & 63);
+        const uint32_t snode = ph - (lo_k >= 0 ? pl : 0u);
+        const bool zero = snode == 0;
+        prm = (zero || !valid) ? 0 : rice_param_exact((uint64_t)snode, len);
+        const unsigned long long eb = __ballot(valid && (zero || prm < 0));
+        if (lane == 0) eflag[0] = eb != 0;
+        if (eb) {
+            const int kl = __builtin_ctzll(eb);
+            mv.status = ST_VALUE;
+            mv.site = __shfl((int)zero, kl) ? FLACMI_SITE_RICE_LOG_DOMAIN : FLACMI_SITE_RICE_NEG_SHIFT;
+            store_meta(meta, lane, mv, coefl);
+        } else {
+            /* the table: finest partition k (lane k) -> the parameter of its ancestor at
+             * every order, as p | p << 16 */
+            int pmax = 0;
+            /* (opaque: lane * 16 bytes would otherwise be shared with the staging's kFixB offset and
+             * held, or spilled, across the whole kernel) */
+            uint16_t* const prow = pkw + (int)opaque((uint32_t)lane) * RS;
+#pragma unroll
+            for (int o2 = 0; o2 < kRiceOrders; ++o2) {
+                if (o2 >= ro && o2 <= oo) {
+                    const int node = (1 << o2) + (lane >> (oo - o2));
+                    const int pv = __shfl(prm, (node - 1) & 63);
+                    pmax = max(pmax, pv);
+                    if (lane < P) prow[o2] = (uint16_t)pv;
+                }
+            }
+            /* bit 15 of a row's entry 0 (order 0's parameter, or unused when rmin > 0): some order's
+             * parameter is >= 16, which v_pk_lshrrev_b16 would take mod 16, so the row's chunks take
+             * the 32-bit path (possible only where a partition's mean is >= 2^16 while one of its
+             * chunks stays below 2^16) */
+            if (lane < P) {
+                if (ro > 0) prow[0] = pmax >= 16 ? 0x8000u : 0u;
+                else if (pmax >= 16) prow[0] |= 0x8000u;
+            }
         }
     }
-    /* bit 15 of a row's entry 0 (order 0's parameter, or unused when rmin > 0): some order's
-     * parameter is >= 16, which v_pk_lshrrev_b16 would take mod 16, so the row's chunks take
-     * the 32-bit path (possible only where a partition's mean is >= 2^16 while one of its
-     * chunks stays below 2^16) */
-    if (lane < P) {
-        if (ro > 0) prow[0] = pmax >= 16 ? 0x8000u : 0u;
-        else if (pmax >= 16) prow[0] |= 0x8000u;
-    }
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads(); /* B3b: the table and the error flag */
+    if (eflag[0]) return; /* workgroup-uniform */
     /* data bits: sum of x >> p over the residual for every candidate order */
     uint32_t tb[kRiceOrders];
 #pragma unroll
