@@ -135,11 +135,13 @@ __device__ __forceinline__ void lpc_finish(const double (&acc)[LMAX + 1], const 
 /* ACF_IN: the autocorrelation is read from a.acf ([count][33]) instead of computed from
  * samples -- the entry point flacmi_device_lpc_from_acf uses to drive Levinson-Durbin and
  * the quantiser into the overflow sites integer PCM never reaches. */
-/* three waves per SIMD for the common orders (L <= 12: <= 168 VGPRs) */
-constexpr int lpc_waves(int lmax) { return lmax <= 12 ? 3 : 1; }
+/* three waves per SIMD for the common orders (L <= 12: <= 168 VGPRs); two for 32-bit samples
+ * at L = 32 (208 VGPRs: the ring cycles of the two tapers and of the rectangle run as three
+ * loops, one path each; with one loop holding both paths the allocator needed > 256) */
+constexpr int lpc_waves(int lmax, int sample_bytes = 4) { return lmax <= 12 ? 3 : sample_bytes == 4 ? 2 : 1; }
 
 template <int LMAX, typename SampleT, bool ACF_IN = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(LMAX)))) void k_lpc(LpcArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(LMAX, (int)sizeof(SampleT))))) void k_lpc(LpcArgs a) {
     const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (gid >= a.count) return;
     const int64_t u = a.unit0 + gid;
@@ -225,14 +227,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
             }
         };
         if (ncyc > 0) loadg(0, gc);
-        for (int c = 0; c < ncyc; ++c) {
+        /* one ring cycle (S samples); RECT: inside the window's rectangle (see below) */
+        auto cycle = [&](int c, auto rectc) __attribute__((always_inline)) {
+            constexpr bool RECT = decltype(rectc)::value;
             const int m0 = c * S;
-            const bool rect = m0 - LMAX >= a.fuse_lo && m0 + S <= a.fuse_hi;
 #pragma unroll
             for (int g = 0; g < S / G; ++g) {
                 const int mg = m0 + g * G;
                 loadg(mg + G, gn);
-                if (rect) { /* exact integer products: one fused op per term (see below) */
+                if constexpr (RECT) { /* exact integer products: one fused op per term (see below) */
 #pragma unroll
                     for (int k = 0; k < G; ++k) {
                         const int t = g * G + k;
@@ -257,7 +260,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
 #pragma unroll
                 for (int k = 0; k < G; ++k) gc[k] = gn[k];
             }
-        }
+        };
+        /* the cycles inside the rectangle form one run [c1, c2): three loops, one path each */
+        int c1 = (a.fuse_lo + LMAX + S - 1) / S;
+        if (a.fuse_lo + LMAX <= 0) c1 = 0;
+        int c2 = a.fuse_hi / S; /* c * S + S <= fuse_hi  <=>  c < fuse_hi / S */
+        if (c2 > ncyc) c2 = ncyc;
+        if (c1 > c2) c1 = c2;
+        using T0 = std::integral_constant<bool, false>;
+        using T1 = std::integral_constant<bool, true>;
+        for (int c = 0; c < c1; ++c) cycle(c, T0{});
+        for (int c = c1; c < c2; ++c) cycle(c, T1{});
+        for (int c = c2; c < ncyc; ++c) cycle(c, T0{});
     } else {
     if (nblk > 0) load(0, cur);
     for (int b = 0; b < nblk; ++b) {
