@@ -170,7 +170,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
 #pragma unroll
     for (int l = 0; l <= LMAX; ++l) acc[l] = 0.0;
     const int M = n - 1; /* the last sample never enters a product (encoder.py:449) */
-    const double* __restrict__ win = a.window;
+    /* the window through the constant address space: scalar loads (a global pointer gets
+     * per-lane vector loads, each waited for with vmcnt(0) -- which also waits for the
+     * samples prefetched a cycle ahead) */
+    const __attribute__((address_space(4))) double* win = (const __attribute__((address_space(4))) double*)a.window;
     /* Samples arrive in load blocks of SB per lane (64 B: a whole half cache line per row
      * per visit), kept packed (int16 pairs) and prefetched one block ahead; each block is
      * processed as SB / S ring-aligned sub-blocks of S samples. */
@@ -209,14 +212,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
     if constexpr (PK == 1) {
         /* 32-bit samples (L up to 32, S = 40): loading whole S-sample blocks would hold 2 x 40
          * sample registers beside the 33 accumulators and the 40-slot ring (one wave per SIMD,
-         * accumulators spilled to AGPRs).  Instead groups of G samples are prefetched one group
-         * ahead while the ring cycles through its S slots (static indices throughout). */
+         * accumulators spilled to AGPRs).  Instead groups of G samples are prefetched one ring
+         * cycle ahead while the ring cycles through its S slots (static indices throughout). */
         constexpr int G = 8;
         static_assert(S % G == 0, "ring length a multiple of the load group");
         const int ncyc = (M + S - 1) / S;
-        uint32_t gc[G], gn[G];
-        auto loadg = [&](int m0, uint32_t (&v)[G]) __attribute__((always_inline)) {
-            if (m0 + G <= M) {
+        /* FULL: the group lies inside [0, M) (the caller knows; no branch, so the waits the
+         * compiler places before each use count only the loads issued since) */
+        auto loadg = [&](int m0, uint32_t (&v)[G], auto fullc) __attribute__((always_inline)) {
+            if (decltype(fullc)::value || m0 + G <= M) {
                 const uint4 q0 = *reinterpret_cast<const uint4*>(x + m0);
                 const uint4 q1 = *reinterpret_cast<const uint4*>(x + m0 + 4);
                 v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w;
@@ -226,20 +230,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
                 for (int k = 0; k < G; ++k) v[k] = (m0 + k < M) ? (uint32_t)x[m0 + k] : 0u;
             }
         };
-        if (ncyc > 0) loadg(0, gc);
-        /* one ring cycle (S samples); RECT: inside the window's rectangle (see below) */
-        auto cycle = [&](int c, auto rectc) __attribute__((always_inline)) {
+        using T0 = std::integral_constant<bool, false>;
+        using T1 = std::integral_constant<bool, true>;
+        /* the samples of one whole ring cycle in flight: group g of cycle c + 1 is loaded into
+         * gb[g] as soon as cycle c has used it (an HBM round trip is longer than one group's
+         * 8 x 33 f64 operations at two waves per SIMD) */
+        uint32_t gb[S / G][G];
+#pragma unroll
+        for (int g = 0; g < S / G; ++g) loadg(g * G, gb[g], T0{});
+        __builtin_amdgcn_s_waitcnt(0x0F70); /* vmcnt(0): the loops below enter with nothing in flight */
+        /* one ring cycle (S samples); RECT: inside the window's rectangle (see below); FULL:
+         * the next cycle lies inside [0, M) */
+        auto cycle = [&](int c, auto rectc, auto fullc) __attribute__((always_inline)) {
             constexpr bool RECT = decltype(rectc)::value;
             const int m0 = c * S;
 #pragma unroll
             for (int g = 0; g < S / G; ++g) {
                 const int mg = m0 + g * G;
-                loadg(mg + G, gn);
                 if constexpr (RECT) { /* exact integer products: one fused op per term (see below) */
 #pragma unroll
                     for (int k = 0; k < G; ++k) {
                         const int t = g * G + k;
-                        const double av = (double)(int32_t)gc[k];
+                        const double av = (double)(int32_t)gb[g][k];
                         ring[t] = av;
 #pragma unroll
                         for (int l = 0; l <= LMAX; ++l) acc[l] = __builtin_fma(ring[(t - l + S) % S], av, acc[l]);
@@ -248,7 +260,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
 #pragma unroll
                     for (int k = 0; k < G; ++k) {
                         const int t = g * G + k;
-                        const double av = (double)(int32_t)gc[k] * win[mg + k];
+                        const double av = (double)(int32_t)gb[g][k] * win[mg + k];
                         ring[t] = av;
 #pragma unroll
                         for (int l = 0; l <= LMAX; ++l) {
@@ -257,21 +269,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
                         }
                     }
                 }
-#pragma unroll
-                for (int k = 0; k < G; ++k) gc[k] = gn[k];
+                /* pinned here: left to itself the scheduler sinks the loads to the end of the
+                 * cycle, and the next cycle then waits on them at once */
+                __builtin_amdgcn_sched_barrier(0);
+                loadg(mg + S, gb[g], fullc);
+                __builtin_amdgcn_sched_barrier(0);
             }
         };
-        /* the cycles inside the rectangle form one run [c1, c2): three loops, one path each */
+        /* Cycles c < cf prefetch a whole cycle inside [0, M).  Among them the rectangle's cycles
+         * form one run [c1, c2); the taper cycles before and after it share one loop (one copy
+         * of the code); the last cycles (c >= cf) take the multiply-and-add path, which is the
+         * reference's own arithmetic and so exact inside the rectangle too. */
+        const int cf = M / S - 1 > 0 ? M / S - 1 : 0;
         int c1 = (a.fuse_lo + LMAX + S - 1) / S;
         if (a.fuse_lo + LMAX <= 0) c1 = 0;
         int c2 = a.fuse_hi / S; /* c * S + S <= fuse_hi  <=>  c < fuse_hi / S */
-        if (c2 > ncyc) c2 = ncyc;
+        if (c2 > cf) c2 = cf;
         if (c1 > c2) c1 = c2;
-        using T0 = std::integral_constant<bool, false>;
-        using T1 = std::integral_constant<bool, true>;
-        for (int c = 0; c < c1; ++c) cycle(c, T0{});
-        for (int c = c1; c < c2; ++c) cycle(c, T1{});
-        for (int c = c2; c < ncyc; ++c) cycle(c, T0{});
+        const int ntap = c1 + (cf - c2);
+        for (int i = 0; i < c1; ++i) cycle(i, T0{}, T1{});
+        for (int c = c1; c < c2; ++c) cycle(c, T1{}, T1{});
+        for (int c = c2; c < cf; ++c) cycle(c, T0{}, T1{});
+        (void)ntap;
+        for (int c = cf; c < ncyc; ++c) cycle(c, T0{}, T0{});
     } else {
     if (nblk > 0) load(0, cur);
     for (int b = 0; b < nblk; ++b) {
