@@ -355,7 +355,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
  * wave (no bank conflicts); the DMA writes lane-linearly, so the rotation is applied to the
  * per-lane SOURCE address. */
 template <int LMAX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(LMAX)))) void k_lpc_tile(LpcArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMAX <= 12 ? 4 : 1))) void k_lpc_tile(LpcArgs a) {
     __shared__ __align__(16) uint4 tiles[4 * 512];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t wave0 = (int64_t)blockIdx.x * 256 + wid * 64;
@@ -404,13 +404,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
     /* this lane's row in the image: segment k at slot 8 lane + ((k - lane) & 7) */
     const uint4* myrow = tile + 8 * lane;
     const int rot = (-lane) & 7;
-    if (ntile > 0) issue(0);
-    for (int tI = 0; tI < ntile; ++tI) {
+    using T0 = std::integral_constant<bool, false>;
+    using T1 = std::integral_constant<bool, true>;
+    /* one 64-sample tile; RECT: the whole tile lies inside the window's rectangle and below M */
+    auto tile_body = [&](int tI, auto rectc) __attribute__((always_inline)) {
+        constexpr bool RECT = decltype(rectc)::value;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* this wave's copies have landed */
         /* two halves of 32 samples; the next tile's copies go out once the second half is
          * read out of the image (they land behind its f64 work) */
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+            /* (a fence per half: hoisted, the 64 window values' scalar loads spill SGPRs) */
+            __builtin_amdgcn_sched_barrier(0);
             const int m0 = (tI << 6) + 32 * h;
             uint32_t v[16];
 #pragma unroll
@@ -422,7 +427,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* read out before the copies overwrite it */
                 if (tI + 1 < ntile) issue((tI + 1) << 6);
             }
-            if (m0 + 32 > M) { /* the last samples: those >= M are zero, as k_lpc loads them */
+            if (!RECT && m0 + 32 > M) { /* the last samples: those >= M are zero, as k_lpc loads them */
 #pragma unroll
                 for (int w = 0; w < 16; ++w) {
                     const int m = m0 + 2 * w;
@@ -432,7 +437,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
 #pragma unroll
             for (int sb = 0; sb < 32 / S; ++sb) {
                 const int ms = m0 + sb * S;
-                if (ms - LMAX >= a.fuse_lo && ms + S <= a.fuse_hi) {
+                if constexpr (RECT) {
                     /* inside the Tukey rectangle: exact integer products, one FMA per term (k_lpc) */
 #pragma unroll
                     for (int t = 0; t < S; ++t) {
@@ -442,7 +447,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
 #pragma unroll
                         for (int l = 0; l <= LMAX; ++l) acc[l] = __builtin_fma(ring[(t - l + S) % S], av, acc[l]);
                     }
-                } else {
+                } else { /* the reference's multiply and add (exact inside the rectangle too) */
 #pragma unroll
                     for (int t = 0; t < S; ++t) {
                         const int i = sb * S + t;
@@ -458,7 +463,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(lpc_waves(L
                 }
             }
         }
-    }
+    };
+    /* the rectangle's whole tiles [t1, t2) between the two tapers: three loops, one path each
+     * (one loop holding both paths needs more registers: 154 VGPRs against 128 here) */
+    int t1 = (a.fuse_lo + LMAX + 63) >> 6;
+    if (a.fuse_lo + LMAX <= 0) t1 = 0;
+    int t2 = min(a.fuse_hi, M) >> 6; /* (tI + 1) * 64 <= min(fuse_hi, M) */
+    if (t2 > ntile) t2 = ntile;
+    if (t1 > t2) t1 = t2;
+    if (ntile > 0) issue(0);
+    for (int tI = 0; tI < t1; ++tI) tile_body(tI, T0{});
+    for (int tI = t1; tI < t2; ++tI) tile_body(tI, T1{});
+    for (int tI = t2; tI < ntile; ++tI) tile_body(tI, T0{});
     if (a.acf) {
         double* o = a.acf + gid * 33;
 #pragma unroll
