@@ -70,6 +70,7 @@ MODE_RICE_ONLY = 3
 KIND_FIXED = 0
 KIND_LPC = 1
 FLAG_ALL_CANDIDATES = 1  # params.reserved[1]: exact sums for every LPC candidate (no pruning)
+FLAG_TIERS_ONLY = 2  # params.reserved[1]: prune with the partial-sum tiers alone (diagnostic)
 LPC_PRUNED = -1          # meta.lpc_order / lpc_sum of a unit whose LPC candidates were pruned
 
 

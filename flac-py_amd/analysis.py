@@ -17,16 +17,18 @@ from ._lib import FlacmiError, check, load
 
 
 def make_params(max_lpc_order: int, qlp_precision: int, rice_min: int, rice_max: int,
-                mode: int = abi.MODE_REFERENCE, all_candidates: bool = False) -> abi.Params:
+                mode: int = abi.MODE_REFERENCE, all_candidates: bool = False,
+                tiers_only: bool = False) -> abi.Params:
     """all_candidates: exact sum(|r|) for every LPC candidate (meta.lpc_order / lpc_sum always
-    exact); by default a unit whose LPC candidates provably lose reports abi.LPC_PRUNED there."""
+    exact); by default a unit whose LPC candidates provably lose reports abi.LPC_PRUNED there.
+    tiers_only (diagnostic): the int8-MFMA path prunes with its partial-sum tiers alone."""
     p = abi.Params()
     p.max_lpc_order = max_lpc_order
     p.qlp_precision = qlp_precision
     p.rice_min = rice_min
     p.rice_max = rice_max
     p.mode = mode
-    p.reserved[1] = abi.FLAG_ALL_CANDIDATES if all_candidates else 0
+    p.reserved[1] = (abi.FLAG_ALL_CANDIDATES if all_candidates else 0) | (abi.FLAG_TIERS_ONLY if tiers_only else 0)
     return p
 
 

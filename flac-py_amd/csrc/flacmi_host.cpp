@@ -411,6 +411,16 @@ static int use_stream() {
     return v;
 }
 
+/* FLACMI_NO_SIGNBOUND=1 prunes the int8-MFMA path with the partial-sum tiers alone, as
+ * FLACMI_FLAG_TIERS_ONLY does per call (A/B runs). */
+static int sign_bound_allowed() {
+    static const int v = [] {
+        const char* e = getenv("FLACMI_NO_SIGNBOUND");
+        return (e && atoi(e) != 0) ? 0 : 1;
+    }();
+    return v;
+}
+
 /* FLACMI_NO_PRUNE=1 computes every LPC candidate's exact sum in reference mode, as
  * FLACMI_FLAG_ALL_CANDIDATES does per call (comparison runs). */
 static int prune_allowed() {
@@ -530,6 +540,7 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.stream = use_stream();
         a.prune = p->mode == FLACMI_MODE_REFERENCE && !o->lpc_sums && !(p->reserved[1] & FLACMI_FLAG_ALL_CANDIDATES) &&
                   prune_allowed();
+        a.sign_bound = !(p->reserved[1] & FLACMI_FLAG_TIERS_ONLY) && sign_bound_allowed();
         const bool wide = needs_wide(k.n, b->sample_bits, L, p->qlp_precision, p->mode);
         int path = (wide || o->residual_bytes == 8) ? 2 : (b->sample_bytes == 2 && p->qlp_precision <= 16) ? 0 : 1;
         if (path == 2 && o->residual_bytes == 4 && split_ok(b->sample_bits, L, p->qlp_precision)) path = 3;

@@ -592,10 +592,17 @@ template <int LMAX, bool PIPE = true>
 __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const unsigned char* pl, int PLB,
                                                    const int32_t* cfl, const int32_t* lsh, int L, int n, int G,
                                                    int tid, int NT, int lane, int wid, int nw,
-                                                   unsigned long long* red, bool prune, int dbg) {
+                                                   unsigned long long* red, bool prune, int dbg, bool sbound) {
     using CT = CoefTables<LMAX>;
     constexpr int NSUM = 5 + LMAX;
     constexpr int NTMAX = (LMAX + 15) / 16;
+    unsigned long long* const red_alt = red + nw * NSUM; /* the second copy of the tier sums */
+    /* the sign-correlation bound (below): K_j over R = [LMAX, n), a thread's chunks summed in
+     * 32 bits (at most four 8-sample chunks of |x| <= 2^23.01 per thread: |part| < 2^28.01) */
+    const bool sb = prune && sbound && dbg < 13 && n <= 32 * NT;
+    int32_t kc[LMAX + 1], kneg = 0;
+#pragma unroll
+    for (int j = 0; j <= LMAX; ++j) kc[j] = 0;
     /* fixed orders on the VALU */
     {
         uint64_t fa[5] = {0, 0, 0, 0, 0};
@@ -611,6 +618,27 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
 #pragma unroll
                 for (int e = 0; e < 4; ++e) x12[4 * g + e] = v[e];
             }
+            if (sb && i0 >= LMAX) {
+                /* w_i = +1 (x_i >= 0) or -1 (x_i < 0) with m_i = x_i >> 31: w_i x = (x ^ m_i) - m_i,
+                 * so sum_i w_i x_{i-j} = sum_i (x_{i-j} ^ m_i) + #{m_i = -1}: one v_xad_u32 each */
+                int32_t xw[LMAX + 8]; /* samples i0 - LMAX .. i0 + 7 */
+                const int4v* wsrc = reinterpret_cast<const int4v*>(xs32 + i0 - LMAX);
+#pragma unroll
+                for (int g = 0; g < LMAX / 4 - 1; ++g) {
+                    const int4v v = wsrc[g];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) xw[4 * g + e] = v[e];
+                }
+#pragma unroll
+                for (int e = 0; e < 12; ++e) xw[LMAX - 4 + e] = x12[e];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int32_t m = xw[LMAX + k] >> 31;
+                    kneg -= m;
+#pragma unroll
+                    for (int j = 0; j <= LMAX; ++j) kc[j] = (int32_t)(((uint32_t)xw[LMAX + k - j] ^ (uint32_t)m) + (uint32_t)kc[j]);
+                }
+            }
             /* a chunk's sums in 32 bits (|x| <= 2^23 on this path: 8 |D4| < 2^30), so each |D|
              * is one v_sad_u32 into its accumulator; 64 bits once per chunk and order */
             uint32_t ca[5] = {0, 0, 0, 0, 0};
@@ -624,6 +652,76 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
             const uint64_t v = wave_sum_u64(fa[o]);
             if (lane == 0) red[wid * NSUM + o] = v;
         }
+    }
+    uint64_t fmin = ~0ull; /* the best exact fixed sum (read at the first test) */
+    auto read_fmin = [&]() __attribute__((always_inline)) {
+        uint64_t tf = 0;
+        if (lane < 5)
+            for (int w2 = 0; w2 < nw; ++w2) tf += red[w2 * NSUM + lane];
+#pragma unroll
+        for (int o = 0; o < 5; ++o) {
+            const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tf >> 32), o) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tf, o);
+            fmin = v < fmin ? v : fmin;
+        }
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tf >> 32), 0) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tf, 0); /* the order-0 sum */
+    };
+    if (sb) {
+        /* The sign-correlation bound.  For any weights |w_i| <= 1 and the residual r of order p
+         * (encoder.py:537-548: r_i = x_i - floor(P_i / 2^s), P_i = sum_j c_j x_{i-j}):
+         *   sum_{i >= p} |r_i| >= sum_{i in R} w_i r_i >= K_0 - (sum_j c_j K_j) / 2^s - N_-,
+         * with R = [LMAX, n) (inside every order's residual range), K_j = sum_{i in R} w_i
+         * x_{i-j} and N_- = #{i in R: w_i = -1} (w_i = -1 turns -floor(P/2^s) into at most
+         * P/2^s - 1 below).  With w_i = sign(x_i) the bound sits within a few percent of the
+         * exact sum whenever the residual follows the signal -- flac-py's negated predictor
+         * makes r ~ 2x -- and K_j costs (LMAX + 1) v_xad_u32 per sample instead of
+         * the LPC tiles.  When every order's bound exceeds the best fixed sum, LPC can neither
+         * win nor tie (encoder.py:135-157); a coefficient-less order ((), 0) has r = x over
+         * the whole unit, whose sum is the fixed order-0 sum exactly. */
+#pragma unroll
+        for (int j = 0; j <= LMAX; ++j) {
+            int32_t v = kc[j];
+            v = (int32_t)((uint32_t)v + dpp_u32<0xB1, 0xf>((uint32_t)v)); /* four lanes: |v| < 2^30.01 */
+            v = (int32_t)((uint32_t)v + dpp_u32<0x4E, 0xf>((uint32_t)v));
+            uint64_t w = (uint64_t)(int64_t)v;
+            w = dpp_add_u64<0x141, 0xf>(w);
+            w = dpp_add_u64<0x140, 0xf>(w);
+            w = dpp_add_u64<0x142, 0xa>(w);
+            w = dpp_add_u64<0x143, 0xc>(w);
+            if (lane == 63) red_alt[wid * NSUM + j] = w;
+        }
+        {
+            const uint32_t v = wave_sum_u32((uint32_t)kneg);
+            if (lane == 0) red_alt[wid * NSUM + LMAX + 1] = v;
+        }
+        __syncthreads();
+        const uint64_t f0 = read_fmin();
+        int64_t kt = 0; /* lane j <= LMAX: K_j; lane LMAX + 1: N_- */
+        if (lane <= LMAX + 1)
+            for (int w2 = 0; w2 < nw; ++w2) kt += (int64_t)red_alt[w2 * NSUM + lane];
+        auto lane64 = [&](int64_t v, int l) __attribute__((always_inline)) -> int64_t {
+            return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l));
+        };
+        const int64_t k0 = lane64(kt, 0) + lane64(kt, LMAX + 1), nneg = lane64(kt, LMAX + 1);
+        /* lane p - 1: order p's bound (coefficients c_{p,1..p} = cfl[(p - 1) CPAD + 0 .. p - 1]) */
+        int64_t S = 0;
+        const int pl = lane + 1;
+#pragma unroll 1
+        for (int j = 1; j <= L; ++j) {
+            const int64_t kj = lane64(kt, j) + nneg;
+            const int32_t c = (pl <= L && j <= pl) ? cfl[lane * CT::CPAD + j - 1] : 0;
+            S += (int64_t)c * kj;
+        }
+        bool lose = true; /* this lane's order provably loses */
+        if (pl <= L) {
+            const int s = lsh[pl - 1], start = lsh[LMAX + pl - 1];
+            if (start == 0) lose = f0 > fmin; /* ((), 0): r = x, the fixed order-0 sum */
+            else lose = k0 - (S >> s) - 1 - nneg > (int64_t)fmin;
+        }
+        if (__ballot(!lose) == 0) return 0x100; /* decided before any LPC tile (meta.lpc_tiers 0/8) */
+        __syncthreads(); /* every wave has read red_alt before a tier writes it */
     }
     const int col = lane & 15, qq = lane >> 4, sg = qq >> 1, h = qq & 1, m = col;
     /* B operands and per-column constants */
@@ -811,12 +909,10 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
     }
     bool pruned = false;
     int done = 0;
-    uint64_t fmin = ~0ull; /* the best exact fixed sum (read at the first test) */
     /* tier t stores its running sums into red when 7 - t is even (the last tier's exact sums
      * land where phase D reads them), else into the copy after it: a wave that starts the
      * next tier stores while slower waves may still read this one's, so a test needs one
      * barrier, not two */
-    unsigned long long* const red_alt = red + nw * NSUM;
     /* eighths of the wave's tiles, spread over the block (residues 0, 4, 2, 6, 1, 5, 3, 7 of
      * the wave's tile index mod 8): a unit stops at the first eighth whose partial LPC sums
      * all exceed the best fixed sum (config 3: LPC sums run ~4x the fixed ones, so most
@@ -837,17 +933,7 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
         done = t + 1;
         if (t == kTiers - 1) break; /* every tile done: the sums are exact */
         __syncthreads();
-        if (fmin == ~0ull) { /* first test: the fixed sums (exact, stored before the tiers) */
-            uint64_t tf = 0;
-            if (lane < 5)
-                for (int w2 = 0; w2 < nw; ++w2) tf += red[w2 * NSUM + lane];
-#pragma unroll
-            for (int o = 0; o < 5; ++o) {
-                const uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tf >> 32), o) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tf, o);
-                fmin = v < fmin ? v : fmin;
-            }
-        }
+        if (fmin == ~0ull) read_fmin(); /* first test: the fixed sums (exact, stored before the tiers) */
         uint64_t tj = 0;
         if (lane >= 5 && lane < 5 + L)
             for (int w2 = 0; w2 < nw; ++w2) tj += buf[w2 * NSUM + lane];
@@ -1552,7 +1638,8 @@ next_unit:
         if constexpr (MF8)
         {
             const int r = mf8_candidate_sums<LMAX>(xs32, smem + lay.pl, PLB, cfl, lsh, L, n, mf8_G, tid, NT, lane, wid,
-                                                   nw, red, a.prune != 0 && !lpc_only && !rice_only, a.stop_after);
+                                                   nw, red, a.prune != 0 && !lpc_only && !rice_only, a.stop_after,
+                                                   a.sign_bound != 0);
             lpc_pruned = (r >> 8) != 0;
             lpc_tiers = r ? (r & 0xff) | (8 << 8) : 0;
         }

@@ -128,6 +128,9 @@ enum flacmi_flags {
     /* compute every LPC candidate's exact sum(|r|) in FLACMI_MODE_REFERENCE (meta.lpc_order /
      * lpc_sum always exact).  Without it the analysis may prune: see FLACMI_LPC_PRUNED. */
     FLACMI_FLAG_ALL_CANDIDATES = 1,
+    /* diagnostic: prune with the partial-sum tiers alone (no sign-correlation bound), so a
+     * test reaches the tier decisions on data the bound already settles */
+    FLACMI_FLAG_TIERS_ONLY = 2,
 };
 
 /* meta.lpc_order and meta.lpc_sum of a unit whose LPC candidates were pruned: exact lower

@@ -664,6 +664,30 @@ def _emulate_eighths(x, rec, L, fixed_sums):
     return 8, False
 
 
+def _emulate_sign_bound(x, rec, L, fixed_sums, lmax=32):
+    """The sign-correlation bound of mf8_candidate_sums restated on the oracle's record: with
+    w_i = +1 (x_i >= 0) or -1, K_j = sum_{i in [lmax, n)} w_i x_{i-j}, N = #{w_i = -1} there,
+    order p loses when K_0 - floor(sum_j c_j K_j / 2^s) - 1 - N exceeds the best fixed sum (a
+    coefficient-less order: when the fixed order-0 sum does).  -> True when every order loses."""
+    x = np.asarray(x, dtype=np.int64)
+    n = len(x)
+    w = np.where(x[lmax:] >= 0, 1, -1)
+    K = [int(np.dot(w, x[lmax - j:n - j])) for j in range(L + 1)]
+    nneg = int((w < 0).sum())
+    fmin = int(np.min(fixed_sums))
+    for p in range(1, L + 1):
+        if (int(rec[1]) >> (p - 1)) & 1:
+            if not int(fixed_sums[0]) > fmin:
+                return False
+            continue
+        s = int(rec[2 + p - 1])
+        base = 2 + L + p * (p - 1) // 2
+        S = sum(int(rec[base + j]) * K[j + 1] for j in range(p))
+        if not K[0] - (S >> s) - 1 - nneg > fmin:
+            return False
+    return True
+
+
 def _c3_tier_units(n, q):
     """24-bit units on every side of the eighth-tier decision (explored with
     _emulate_eighths): full-scale tones at noise 0 / 0.5 / 4 and config-3 synthetic units
@@ -704,34 +728,47 @@ def _c3_tier_units(n, q):
 def test_c3_int8_pruning_tiers_vs_oracle(az, n, q):
     """Config-3 production mode (LPC pruning on) on the int8-MFMA path, 24-bit, L = 32,
     r 0..8: every reference-visible field equals the oracle and the all-candidates run, and
-    meta.lpc_tiers (the eighths computed before the decision) equals the decision restated
-    on the oracle's exact candidates.  Each outcome occurs: pruned after two eighths, pruned
-    later, every eighth then fixed, LPC chosen, a near tie, and (n = 4096) the tie
-    AssertionError (encoder.py:133-157)."""
+    meta.lpc_tiers equals the decision restated on the oracle's exact candidates: 0/8 when
+    the sign-correlation bound settles the unit before any LPC tile (_emulate_sign_bound),
+    else the eighths computed before the decision; the tiers-only run (FLACMI_FLAG_TIERS_ONLY)
+    takes the eighths for every unit.  Each outcome occurs: pruned by the sign bound, pruned
+    after two eighths, pruned later, every eighth then fixed, LPC chosen, a near tie, and
+    (n = 4096) the tie AssertionError (encoder.py:133-157)."""
     L = 32
     a = _c3_tier_units(n, q)
     nu = len(a)
     ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, 8), n, sample_bits=24, threads=16)
     prod = az.analyze(a, make_params(L, q, 0, 8), n, sample_bits=24)
+    tier = az.analyze(a, make_params(L, q, 0, 8, tiers_only=True), n, sample_bits=24)
     full = az.analyze(a, make_params(L, q, 0, 8, all_candidates=True), n, sample_bits=24)
     compare_with_oracle(prod, ora, [n] * nu)
+    compare_with_oracle(tier, ora, [n] * nu)
     compare_with_oracle(full, ora, [n] * nu)
     assert (full["meta"]["lpc_tiers"] == 0).all()
-    pm, om = prod["meta"], ora["meta"]
+    pm, tm, om = prod["meta"], tier["meta"], ora["meta"]
     seen = set()
     for u in range(nu):
         _meta_params_residual_equal(prod, full, u)
+        _meta_params_residual_equal(tier, full, u)
         st = int(om["status"][u])
         if st != 0 and int(om["site"][u]) != abi.SITE_CHOICE_TIE:
             continue
-        tiers = int(pm["lpc_tiers"][u])
+        tiers = int(tm["lpc_tiers"][u])
         if not _int8_path(a[u], ora["lpc_records"][u], L):  # the int64 chains: exact, no pruning
-            assert tiers == 0 and int(pm["lpc_order"][u]) != abi.LPC_PRUNED, (u, "int64 path", tiers)
+            assert tiers == 0 and int(tm["lpc_order"][u]) != abi.LPC_PRUNED, (u, "int64 path", tiers)
+            assert int(pm["lpc_tiers"][u]) == 0 and int(pm["lpc_order"][u]) != abi.LPC_PRUNED, (u, "int64 path")
             seen.add("int64")
             continue
         done, pr = _emulate_eighths(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u])
         assert tiers == done | (8 << 8), (u, "lpc_tiers", tiers & 0xff, tiers >> 8, "want", done)
-        assert (int(pm["lpc_order"][u]) == abi.LPC_PRUNED) == pr, (u, "pruned")
+        assert (int(tm["lpc_order"][u]) == abi.LPC_PRUNED) == pr, (u, "pruned")
+        sbp = _emulate_sign_bound(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u])
+        want_prod = (8 << 8) if sbp else done | (8 << 8)
+        assert int(pm["lpc_tiers"][u]) == want_prod, (u, "production lpc_tiers", int(pm["lpc_tiers"][u]), want_prod)
+        assert (int(pm["lpc_order"][u]) == abi.LPC_PRUNED) == (sbp or pr), (u, "pruned (production)")
+        if sbp:
+            assert pr or st == 0 and int(om["lpc_sum"][u]) > int(om["fixed_sum"][u]), (u, "sign bound vs exact sums")
+            seen.add("sign-bound")
         if st != 0:
             seen.add("tie")
         elif pr:
@@ -742,5 +779,5 @@ def test_c3_int8_pruning_tiers_vs_oracle(az, n, q):
             seen.add("exact-fixed")
         if st == 0 and not pr and abs(int(om["lpc_sum"][u]) - int(om["fixed_sum"][u])) <= 1e-3 * int(om["fixed_sum"][u]):
             seen.add("near-tie")
-    want = {"pruned@2", "pruned-later", "exact-fixed", "lpc", "near-tie"} | ({"tie"} if n == 4096 else set())
+    want = {"sign-bound", "pruned@2", "pruned-later", "exact-fixed", "lpc", "near-tie"} | ({"tie"} if n == 4096 else set())
     assert want <= seen, want - seen
