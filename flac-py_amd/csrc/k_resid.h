@@ -697,31 +697,35 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
         }
         __syncthreads();
         const uint64_t f0 = read_fmin();
-        int64_t kt = 0; /* lane j <= LMAX: K_j; lane LMAX + 1: N_- */
-        if (lane <= LMAX + 1)
-            for (int w2 = 0; w2 < nw; ++w2) kt += (int64_t)red_alt[w2 * NSUM + lane];
-        auto lane64 = [&](int64_t v, int l) __attribute__((always_inline)) -> int64_t {
-            return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l));
-        };
-        const int64_t k0 = lane64(kt, 0) + lane64(kt, LMAX + 1), nneg = lane64(kt, LMAX + 1);
-        /* lane p - 1: order p's bound (coefficients c_{p,1..p} = cfl[(p - 1) CPAD + 0 .. p - 1]) */
-        int64_t S = 0;
-        const int pl = lane + 1;
+        if (wid == 0) { /* one wave evaluates the bounds; the others wait for its verdict */
+            int64_t kt = 0; /* lane j <= LMAX: K_j; lane LMAX + 1: N_- */
+            if (lane <= LMAX + 1)
+                for (int w2 = 0; w2 < nw; ++w2) kt += (int64_t)red_alt[w2 * NSUM + lane];
+            auto lane64 = [&](int64_t v, int l) __attribute__((always_inline)) -> int64_t {
+                return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l));
+            };
+            const int64_t k0 = lane64(kt, 0) + lane64(kt, LMAX + 1), nneg = lane64(kt, LMAX + 1);
+            /* lane p - 1: order p's bound (coefficients c_{p,1..p} = cfl[(p - 1) CPAD + 0 .. p - 1]) */
+            int64_t S = 0;
+            const int pl = lane + 1;
 #pragma unroll 1
-        for (int j = 1; j <= L; ++j) {
-            const int64_t kj = lane64(kt, j) + nneg;
-            const int32_t c = (pl <= L && j <= pl) ? cfl[lane * CT::CPAD + j - 1] : 0;
-            S += (int64_t)c * kj;
+            for (int j = 1; j <= L; ++j) {
+                const int64_t kj = lane64(kt, j) + nneg;
+                const int32_t c = (pl <= L && j <= pl) ? cfl[lane * CT::CPAD + j - 1] : 0;
+                S += (int64_t)c * kj;
+            }
+            bool lose = true; /* this lane's order provably loses */
+            if (pl <= L) {
+                const int s = lsh[pl - 1], start = lsh[LMAX + pl - 1];
+                if (start == 0) lose = f0 > fmin; /* ((), 0): r = x, the fixed order-0 sum */
+                else lose = k0 - (S >> s) - 1 - nneg > (int64_t)fmin;
+            }
+            const bool decided = __ballot(!lose) == 0;
+            if (lane == 0) red_alt[LMAX + 2] = decided ? 1ull : 0ull; /* wave 0's unused slot */
         }
-        bool lose = true; /* this lane's order provably loses */
-        if (pl <= L) {
-            const int s = lsh[pl - 1], start = lsh[LMAX + pl - 1];
-            if (start == 0) lose = f0 > fmin; /* ((), 0): r = x, the fixed order-0 sum */
-            else lose = k0 - (S >> s) - 1 - nneg > (int64_t)fmin;
-        }
-        if (__ballot(!lose) == 0) return 0x100; /* decided before any LPC tile (meta.lpc_tiers 0/8) */
-        __syncthreads(); /* every wave has read red_alt before a tier writes it */
+        __syncthreads(); /* the verdict; every wave is past its red_alt reads before a tier writes it */
+        if (red_alt[LMAX + 2] != 0) return 0x100; /* decided before any LPC tile (meta.lpc_tiers 0/8) */
     }
     const int col = lane & 15, qq = lane >> 4, sg = qq >> 1, h = qq & 1, m = col;
     /* B operands and per-column constants */
