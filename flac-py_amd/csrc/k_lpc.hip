@@ -484,112 +484,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LMAX <= 12 
 }
 
 
-/* k_lpc_2p: 32-bit samples at L = 32 in two passes over the unit's samples, lags 0..16 then
- * 17..32, each with its own accumulators (17 / 16 doubles) and a ring just long enough for
- * its lags (24 / 40 slots): the same per-lag chains as k_lpc (bit-identical), with no pass
- * holding the 40-slot ring beside all 33 accumulators, so the kernel fits two waves per SIMD
- * (k_lpc at L = 32 needs 256 VGPRs + 28 AGPRs: one wave per SIMD, and 2e5 units = 3125
- * waves = 3.05 rounds of 1024 SIMDs).  The second pass reads the samples again. */
-template <int LMAX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_lpc_2p(LpcArgs a) {
-    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (gid >= a.count) return;
-    const int64_t u = a.unit0 + gid;
-    const int32_t* __restrict__ x = (const int32_t*)a.samples + u * a.stride;
-    int32_t* __restrict__ rec = a.rec + gid * a.rec_words;
-    const int n = a.n, L = a.L;
-    constexpr int LS = (LMAX + 2) / 2; /* lags 0 .. LS-1, then LS .. LMAX */
-    double acc[LMAX + 1];
-    if (n >= 4 && n <= 7) { /* tukey: nr == 0 -> pi * 0 / 0 (encoder.py:437) */
-        rec[0] = ST_ZERODIV | (FLACMI_SITE_TUKEY << 16);
-        rec[1] = 0;
-        if (a.acf)
-            for (int l = 0; l < 33; ++l) a.acf[gid * 33 + l] = 0.0;
-        return;
-    }
-    const int M = n - 1; /* the last sample never enters a product (encoder.py:449) */
-    const double* __restrict__ win = a.window;
-    constexpr int G = 8;
-    auto pass = [&](auto LB_, auto LE_, auto S_) __attribute__((always_inline)) {
-        constexpr int LB = decltype(LB_)::value, LE = decltype(LE_)::value, S = decltype(S_)::value;
-        static_assert(S % G == 0 && S >= LE, "ring: a multiple of the load group, every lag");
-        double ring[S], ap[LE - LB];
-#pragma unroll
-        for (int t = 0; t < S; ++t) ring[t] = 0.0;
-#pragma unroll
-        for (int l = 0; l < LE - LB; ++l) ap[l] = 0.0;
-        const int ncyc = (M + S - 1) / S;
-        uint32_t gc[G], gn[G];
-        auto loadg = [&](int m0, uint32_t (&v)[G]) __attribute__((always_inline)) {
-            if (m0 + G <= M) {
-                const uint4 q0 = *reinterpret_cast<const uint4*>(x + m0);
-                const uint4 q1 = *reinterpret_cast<const uint4*>(x + m0 + 4);
-                v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w;
-                v[4] = q1.x; v[5] = q1.y; v[6] = q1.z; v[7] = q1.w;
-            } else {
-#pragma unroll
-                for (int k = 0; k < G; ++k) v[k] = (m0 + k < M) ? (uint32_t)x[m0 + k] : 0u;
-            }
-        };
-        if (ncyc > 0) loadg(0, gc);
-        for (int c = 0; c < ncyc; ++c) {
-            const int m0 = c * S;
-            const bool rect = m0 - LMAX >= a.fuse_lo && m0 + S <= a.fuse_hi;
-#pragma unroll
-            for (int g = 0; g < S / G; ++g) {
-                const int mg = m0 + g * G;
-                loadg(mg + G, gn);
-                if (rect) {
-#pragma unroll
-                    for (int k = 0; k < G; ++k) {
-                        const int t = g * G + k;
-                        const double av = (double)(int32_t)gc[k];
-                        ring[t] = av;
-#pragma unroll
-                        for (int l = LB; l < LE; ++l) ap[l - LB] = __builtin_fma(ring[(t - l + S) % S], av, ap[l - LB]);
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < G; ++k) {
-                        const int t = g * G + k;
-                        const double av = (double)(int32_t)gc[k] * win[mg + k];
-                        ring[t] = av;
-#pragma unroll
-                        for (int l = LB; l < LE; ++l) {
-                            const double prev = ring[(t - l + S) % S];
-                            ap[l - LB] = ap[l - LB] + prev * av;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < G; ++k) gc[k] = gn[k];
-            }
-        }
-#pragma unroll
-        for (int l = LB; l < LE; ++l) acc[l] = ap[l - LB];
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using ILS = std::integral_constant<int, LS>;
-    using IL1 = std::integral_constant<int, LMAX + 1>;
-    pass(I0{}, ILS{}, std::integral_constant<int, ((LS + G - 1) / G) * G>{});
-    pass(ILS{}, IL1{}, std::integral_constant<int, ((LMAX + 1 + G - 1) / G) * G>{});
-    if (a.acf) {
-        double* o = a.acf + gid * 33;
-#pragma unroll
-        for (int l = 0; l < 33; ++l) o[l] = (l <= LMAX && l <= L) ? acc[l < LMAX ? l : LMAX] : 0.0;
-    }
-    lpc_finish<LMAX>(acc, a, rec);
-}
-
-/* FLACMI_LPC_2PASS=1: 32-bit samples at L > 16 through k_lpc_2p (opt-in while measured) */
-static bool lpc_2pass_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("FLACMI_LPC_2PASS");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 /* FLACMI_LPC_TILE=0 selects k_lpc for int16 rows (A/B and parity comparison) */
 static bool lpc_tile_enabled() {
     static const bool on = [] {
@@ -617,12 +511,6 @@ static hipError_t launch_lpc_T(const LpcArgs& a, hipStream_t s) {
             r.rec += full * a.rec_words;
             if (r.acf) r.acf += full * 33;
             hipLaunchKernelGGL((k_lpc<LMAX, int16_t>), dim3((unsigned)((r.count + 255) / 256)), dim3(256), 0, s, r);
-            return hipGetLastError();
-        }
-    }
-    if constexpr (LMAX == 32) {
-        if (a.sample_bytes == 4 && lpc_2pass_enabled()) {
-            hipLaunchKernelGGL((k_lpc_2p<LMAX>), grid, dim3(256), 0, s, a);
             return hipGetLastError();
         }
     }

@@ -1,5 +1,5 @@
 # GPU suite (persistent kVarMf8 default, its copies issued in inline asm), c3 A/B vs
-# FLACMI_MF8_PERSIST=0, and the k_lpc_2p A/B (tools/gpu_r04f.sh).
+# FLACMI_MF8_PERSIST=0 (the k_lpc_2p A/B of that run: kernel since removed).
 set -o pipefail
 TAG=${1:-r04g}
 OUT=gpurun_out/$TAG
@@ -12,4 +12,3 @@ for v in 1 0 1 0; do
   FLACMI_MF8_PERSIST=$v timeout -k 10 200 python bench.py --config c3 $B > $OUT/c3_p$v.json 2> $OUT/c3_p$v.err || { tail -20 $OUT/c3_p$v.err; exit 1; }
   python -c "import json;d=json.load(open('$OUT/c3_p$v.json'));k=d['kernels'];print('c3 MF8_PERSIST=$v', '%.3e'%d['value'], 'lpc %.2f resid %.2f call %.2f'%(k['k_lpc_ms'],k['k_resid_ms'],k['call_ms']), (d.get('parity') or {}).get('mismatches'))"
 done
-bash tools/gpu_r04f.sh $TAG/2p
