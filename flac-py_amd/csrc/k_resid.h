@@ -577,6 +577,14 @@ __device__ __forceinline__ void mf8_tile_epilogue(const v4i (&D)[4], int s, cons
     }
 }
 
+/* (a ^ b) + c in one v_xad_u32 (left to itself the compiler pairs two v_xor_b32 with one
+ * v_add3_u32: 1.5 instructions per term) */
+__device__ __forceinline__ uint32_t xad_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 /* Sums of |r| for LPC orders 1..L (into red[wid][5 + p - 1]) and fixed orders 0..4 (VALU,
  * 8-sample chunks, into red[wid][0..4]).  pl: the three digit planes, PLB bytes apart;
  * cfl / lsh: phase A's coefficient and shift tables; G: tiles per u32 partial sum.
@@ -636,7 +644,7 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
                     const int32_t m = xw[LMAX + k] >> 31;
                     kneg -= m;
 #pragma unroll
-                    for (int j = 0; j <= LMAX; ++j) kc[j] = (int32_t)(((uint32_t)xw[LMAX + k - j] ^ (uint32_t)m) + (uint32_t)kc[j]);
+                    for (int j = 0; j <= LMAX; ++j) kc[j] = (int32_t)xad_u32((uint32_t)xw[LMAX + k - j], (uint32_t)m, (uint32_t)kc[j]);
                 }
             }
             /* a chunk's sums in 32 bits (|x| <= 2^23 on this path: 8 |D4| < 2^30), so each |D|
@@ -679,17 +687,25 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
          * the LPC tiles.  When every order's bound exceeds the best fixed sum, LPC can neither
          * win nor tie (encoder.py:135-157); a coefficient-less order ((), 0) has r = x over
          * the whole unit, whose sum is the fixed order-0 sum exactly. */
+        /* wave sums in 32-bit steps: quads first (|v| < 2^30.01), then the quad sums split as
+         * v = 2^16 hi + lo (lo < 2^16, |hi| < 2^14.01), whose sums over the wave's 16 quads stay
+         * below 2^20 and 2^18.01; the slot holds (hi sum, lo sum) as two words, and the
+         * evaluating wave forms 2^16 hi + lo in 64 bits */
 #pragma unroll
         for (int j = 0; j <= LMAX; ++j) {
-            int32_t v = kc[j];
-            v = (int32_t)((uint32_t)v + dpp_u32<0xB1, 0xf>((uint32_t)v)); /* four lanes: |v| < 2^30.01 */
-            v = (int32_t)((uint32_t)v + dpp_u32<0x4E, 0xf>((uint32_t)v));
-            uint64_t w = (uint64_t)(int64_t)v;
-            w = dpp_add_u64<0x141, 0xf>(w);
-            w = dpp_add_u64<0x140, 0xf>(w);
-            w = dpp_add_u64<0x142, 0xa>(w);
-            w = dpp_add_u64<0x143, 0xc>(w);
-            if (lane == 63) red_alt[wid * NSUM + j] = w;
+            uint32_t v = (uint32_t)kc[j];
+            v += dpp_u32<0xB1, 0xf>(v);
+            v += dpp_u32<0x4E, 0xf>(v);
+            uint32_t lo = v & 0xffffu, hi = (uint32_t)((int32_t)v >> 16);
+            lo += dpp_u32<0x141, 0xf>(lo);
+            hi += dpp_u32<0x141, 0xf>(hi);
+            lo += dpp_u32<0x140, 0xf>(lo);
+            hi += dpp_u32<0x140, 0xf>(hi);
+            lo += dpp_u32<0x142, 0xa>(lo);
+            hi += dpp_u32<0x142, 0xa>(hi);
+            lo += dpp_u32<0x143, 0xc>(lo);
+            hi += dpp_u32<0x143, 0xc>(hi);
+            if (lane == 63) red_alt[wid * NSUM + j] = ((uint64_t)hi << 32) | lo;
         }
         {
             const uint32_t v = wave_sum_u32((uint32_t)kneg);
@@ -699,7 +715,12 @@ __device__ __forceinline__ int mf8_candidate_sums(const int32_t* xs32, const uns
         const uint64_t f0 = read_fmin();
         if (wid == 0) { /* one wave evaluates the bounds; the others wait for its verdict */
             int64_t kt = 0; /* lane j <= LMAX: K_j; lane LMAX + 1: N_- */
-            if (lane <= LMAX + 1)
+            if (lane <= LMAX)
+                for (int w2 = 0; w2 < nw; ++w2) {
+                    const uint64_t v = red_alt[w2 * NSUM + lane];
+                    kt += ((int64_t)(int32_t)(uint32_t)(v >> 32) << 16) + (int64_t)(uint32_t)v;
+                }
+            else if (lane == LMAX + 1)
                 for (int w2 = 0; w2 < nw; ++w2) kt += (int64_t)red_alt[w2 * NSUM + lane];
             auto lane64 = [&](int64_t v, int l) __attribute__((always_inline)) -> int64_t {
                 return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l) << 32) |
