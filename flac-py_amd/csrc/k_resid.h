@@ -1600,40 +1600,50 @@ next_unit:
     if constexpr (MF8) {
         if (a.sample_bytes == 4 && a.mfma && do_lpc && L >= 1 && n % 16 == 0 && n >= 32) {
             /* the unit's bound B on |r| and |floor(pred / 2^s)|, lane-parallel over the
-             * orders (lane p-1) and reduced over the wave: every wave gets the same answer */
-            uint32_t xm = lane < nw ? mf8_xmax[lane] : 0u;
-            uint64_t b = 0;
-            if (lane < L) {
-                const int p = lane + 1;
-                uint32_t sa = 0;
-                bool cok = true;
+             * orders (lane p-1) and reduced over wave 0, whose verdict (int8 path or not, tiles
+             * per u32 partial sum) the other waves read after one barrier */
+            if (wid == 0) {
+                uint32_t xm = lane < nw ? mf8_xmax[lane] : 0u;
+                uint64_t b = 0;
+                if (lane < L) {
+                    const int p = lane + 1;
+                    uint32_t sa = 0;
+                    bool cok = true;
 #pragma unroll
-                for (int j = 0; j < LMAX; ++j) {
-                    const int32_t c = j < p ? cfl[lane * CT::CPAD + j] : 0;
-                    cok &= c <= 32639 && c >= -32640; /* the top coefficient digit fits a byte */
-                    sa += (uint32_t)(c < 0 ? -c : c);
+                    for (int j = 0; j < LMAX; ++j) {
+                        const int32_t c = j < p ? cfl[lane * CT::CPAD + j] : 0;
+                        cok &= c <= 32639 && c >= -32640; /* the top coefficient digit fits a byte */
+                        sa += (uint32_t)(c < 0 ? -c : c);
+                    }
+                    b = cok ? ((uint64_t)sa << 32) | (uint32_t)lsh[lane] : ~0ull;
                 }
-                b = cok ? ((uint64_t)sa << 32) | (uint32_t)lsh[lane] : ~0ull;
-            }
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                const uint32_t t = (uint32_t)__shfl_xor((int)xm, o);
-                xm = t > xm ? t : xm;
-            }
-            uint64_t bl = 0;
-            if (lane < L)
-                bl = b == ~0ull || xm >= (1u << 31) ? ~0ull
-                                                    : (uint64_t)xm + (((b >> 32) * (uint64_t)xm) >> (b & 31)) + 1;
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const uint32_t t = (uint32_t)__shfl_xor((int)xm, o);
+                    xm = t > xm ? t : xm;
+                }
+                uint64_t bl = 0;
+                if (lane < L)
+                    bl = b == ~0ull || xm >= (1u << 31) ? ~0ull
+                                                        : (uint64_t)xm + (((b >> 32) * (uint64_t)xm) >> (b & 31)) + 1;
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                const uint64_t t = (uint64_t)__shfl_xor((unsigned long long)bl, o);
-                bl = t > bl ? t : bl;
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const uint64_t t = (uint64_t)__shfl_xor((unsigned long long)bl, o);
+                    bl = t > bl ? t : bl;
+                }
+                const uint64_t bmax = bl;
+                int v = 0;
+                if ((bmax >> 29) == 0) {
+                    const uint64_t g = 0xffffffffull / (4 * bmax); /* >= 2 under bmax < 2^29 */
+                    v = 1 | ((g > 64 ? 64 : (int)g) << 8);
+                }
+                if (lane == 0) misc[5] = v;
             }
-            const uint64_t bmax = bl;
-            if (__builtin_amdgcn_readfirstlane((int)(bmax >> 29)) == 0) {
+            __syncthreads();
+            const int v = __builtin_amdgcn_readfirstlane(misc[5]);
+            if (v & 1) {
                 use_mf8 = true;
-                const uint64_t g = 0xffffffffull / (4 * bmax); /* >= 2 under bmax < 2^29 */
-                mf8_G = __builtin_amdgcn_readfirstlane(g > 64 ? 64 : (int)g); /* wave-uniform */
+                mf8_G = v >> 8; /* wave-uniform */
             }
         }
     }
