@@ -9,6 +9,7 @@ import pytest
 
 import golden_util as G
 import oracle
+import sign_bound
 from flac_amd import abi
 from flac_amd.analysis import Analyzer, make_params, unit_result
 
@@ -665,27 +666,9 @@ def _emulate_eighths(x, rec, L, fixed_sums):
 
 
 def _emulate_sign_bound(x, rec, L, fixed_sums, lmax=32):
-    """The sign-correlation bound of mf8_candidate_sums restated on the oracle's record: with
-    w_i = +1 (x_i >= 0) or -1, K_j = sum_{i in [lmax, n)} w_i x_{i-j}, N = #{w_i = -1} there,
-    order p loses when K_0 - floor(sum_j c_j K_j / 2^s) - 1 - N exceeds the best fixed sum (a
-    coefficient-less order: when the fixed order-0 sum does).  -> True when every order loses."""
-    x = np.asarray(x, dtype=np.int64)
-    n = len(x)
-    w = np.where(x[lmax:] >= 0, 1, -1)
-    K = [int(np.dot(w, x[lmax - j:n - j])) for j in range(L + 1)]
-    nneg = int((w < 0).sum())
-    fmin = int(np.min(fixed_sums))
-    for p in range(1, L + 1):
-        if (int(rec[1]) >> (p - 1)) & 1:
-            if not int(fixed_sums[0]) > fmin:
-                return False
-            continue
-        s = int(rec[2 + p - 1])
-        base = 2 + L + p * (p - 1) // 2
-        S = sum(int(rec[base + j]) * K[j + 1] for j in range(p))
-        if not K[0] - (S >> s) - 1 - nneg > fmin:
-            return False
-    return True
+    """The sign-correlation bound of mf8_candidate_sums restated on the oracle's record
+    (tests/sign_bound.py) -> True when every order loses to the best fixed sum."""
+    return sign_bound.decides(x, rec, L, fixed_sums, lmax)
 
 
 def _c3_tier_units(n, q):
