@@ -368,14 +368,40 @@ def broadcast_comm_id(cid, dist, nbytes, device=None):
     return bytes(t.cpu().numpy().tobytes())
 
 
+def all_ranks_ok(ok, dist, device=None):
+    """True when `ok` holds on every rank (a MIN all-reduce over the process group)."""
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 def open_stats_comm(az, dist, rank, world, device):
     """The C-ABI stats communicator of an N-rank job: rank 0's id broadcast over the process
-    group, then flacmi_comm_init on every rank (a collective call)."""
+    group, then flacmi_comm_init on every rank (a collective call).  -> (comm, reason): comm
+    None, with the reason, when some rank cannot load RCCL or build the communicator (every
+    rank first asks for an id, which loads RCCL, and all agree before the collective init),
+    so the job reduces through torch.distributed instead of failing."""
     from flac_amd import abi
     from flac_amd.analysis import StatsComm
-    cid = StatsComm.comm_id(az.lib) if rank == 0 else None
-    cid = broadcast_comm_id(cid, dist, abi.COMM_ID_BYTES, device)
-    return StatsComm(az, world, rank, cid)
+    why = ""
+    try:
+        cid = StatsComm.comm_id(az.lib)  # every rank: proves RCCL loads here; rank 0's is used
+    except Exception as e:  # noqa: BLE001 (recorded in the bench line)
+        cid, why = None, f"rank {rank}: flacmi_comm_id: {e}"
+    if not all_ranks_ok(cid is not None, dist, device):
+        return None, why or "a rank could not load RCCL (flacmi_comm_id)"
+    cid = broadcast_comm_id(cid if rank == 0 else None, dist, abi.COMM_ID_BYTES, device)
+    comm = None
+    try:
+        comm = StatsComm(az, world, rank, cid)
+    except Exception as e:  # noqa: BLE001
+        why = f"rank {rank}: flacmi_comm_init: {e}"
+    if not all_ranks_ok(comm is not None, dist, device):
+        if comm is not None:
+            comm.close()
+        return None, why or "a rank could not build the communicator (flacmi_comm_init)"
+    return comm, ""
 
 
 def reduce_elapsed(elapsed, dist=None, device=None):
@@ -515,7 +541,7 @@ def main(argv=None):
     stats_acc = torch.zeros_like(stats)
     bufs = dict(samples=samples, meta=meta, rparams=rparams, residual=residual, stats=stats, stats_acc=stats_acc)
     # N > 1: the stream totals go through the C-ABI collective (flacmi_allreduce_stats)
-    comm = open_stats_comm(az, dist, rank, world, dev) if distributed else None
+    comm, comm_note = open_stats_comm(az, dist, rank, world, dev) if distributed else (None, "")
 
     def step():
         if not chunked:
@@ -541,8 +567,10 @@ def main(argv=None):
         dist.all_reduce(via_torch)
         reduce_stats(local_stats, dist, comm, sptr)
         torch.cuda.synchronize(dev)
-        if not torch.equal(local_stats, via_torch):
-            raise SystemExit(f"rank {rank}: flacmi_allreduce_stats differs from torch.distributed's all_reduce")
+        if not all_ranks_ok(torch.equal(local_stats, via_torch), dist, dev):
+            # recorded in the bench line; the timed steps then reduce through torch.distributed
+            comm.close()
+            comm, comm_note = None, "flacmi_allreduce_stats differed from torch.distributed's all_reduce"
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -636,7 +664,8 @@ def main(argv=None):
                        "units_total": total_units, "chunk_units": units if chunked else None, "block": n, "sample_bits": bits,
                        "max_lpc_order": cfg["L"], "qlp_precision": cfg["q"], "rice": [cfg["rmin"], cfg["rmax"]],
                        "mode": "fixed-only" if cfg["mode"] else "reference", "parallelism": f"dp{world} (block shards)",
-                       "stats_collective": "flacmi_allreduce_stats (C-ABI, RCCL)" if comm is not None else None},
+                       "stats_collective": ("flacmi_allreduce_stats (C-ABI, RCCL)" if comm is not None else
+                                            f"torch.distributed all_reduce ({comm_note})" if distributed else None)},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": dom_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dom_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": (os.path.relpath(tfile, REPO) + ": rocprofv3 FETCH_SIZE/WRITE_SIZE passes "

@@ -153,3 +153,43 @@ def test_reduce_stats_routes_through_the_c_abi_comm():
     c = Comm()
     assert bench.reduce_stats(st, None, c, 1234) is st
     assert c.calls == [(st.data_ptr(), 1234)]
+
+
+def _comm_worker(rank, world, port, out):
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    import bench
+
+    class _NoRccl:  # an analyzer whose library cannot hand out an RCCL id on this rank
+        class lib:  # noqa: N801
+            @staticmethod
+            def flacmi_comm_id(buf):
+                return -5 if rank == 1 else 0
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        comm, why = bench.open_stats_comm(_NoRccl(), dist, rank, world, None)
+        out.put((rank, comm is None, why))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_open_stats_comm_falls_back_together():
+    """When one rank cannot load RCCL (flacmi_comm_id fails there), every rank learns it
+    before the collective flacmi_comm_init and returns no communicator, so the N-rank bench
+    reduces through torch.distributed instead of hanging or failing (the reason goes into
+    the bench line's config.stats_collective)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(none for _, none, _ in res)
+    assert "rank 1" in res[1][2] and "flacmi_comm_id" in res[1][2]
+    assert res[0][2]  # rank 0 reports why too
