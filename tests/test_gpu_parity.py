@@ -665,10 +665,18 @@ def _emulate_eighths(x, rec, L, fixed_sums):
     return 8, False
 
 
-def _emulate_sign_bound(x, rec, L, fixed_sums, lmax=32):
-    """The sign-correlation bound of mf8_candidate_sums restated on the oracle's record
-    (tests/sign_bound.py) -> True when every order loses to the best fixed sum."""
-    return sign_bound.decides(x, rec, L, fixed_sums, lmax)
+def _sb_lean(n, rmax=8):
+    """k_resid.h launch_resid_sb's shapes (k_resid_sb, which tests the bound first over each
+    thread's first chunk: R' = [lmax, 4096) with 512 threads)."""
+    om = max(o for o in range(0, rmax + 1) if n % (1 << o) == 0)
+    cpp = (n >> om) // 8
+    return 8192 <= n <= 16384 and n % 256 == 0 and 6 <= om <= 8 and (n >> om) % 8 == 0 and cpp & (cpp - 1) == 0
+
+
+def _emulate_sign_bound(x, rec, L, fixed_sums, lmax=32, lean=False):
+    """The sign-correlation bound of mf8_candidate_sums / k_resid_sb restated on the oracle's
+    record (tests/sign_bound.py) -> True when every order loses to the best fixed sum."""
+    return sign_bound.decides(x, rec, L, fixed_sums, lmax, split_end=8 * 1 * 512 if lean else None)
 
 
 def _c3_tier_units(n, q):
@@ -706,9 +714,9 @@ def _c3_tier_units(n, q):
     return np.ascontiguousarray(np.concatenate(rows))
 
 
-@pytest.mark.parametrize("q", [15, 12])
-@pytest.mark.parametrize("n", [16384, 4096])
-def test_c3_int8_pruning_tiers_vs_oracle(az, n, q):
+@pytest.mark.parametrize("n,q,L", [(16384, 15, 32), (16384, 12, 32), (4096, 15, 32), (4096, 12, 32),
+                                   (16384, 15, 16), (16384, 15, 20), (4096, 15, 16)])
+def test_c3_int8_pruning_tiers_vs_oracle(az, n, q, L):
     """Config-3 production mode (LPC pruning on) on the int8-MFMA path, 24-bit, L = 32,
     r 0..8: every reference-visible field equals the oracle and the all-candidates run, and
     meta.lpc_tiers equals the decision restated on the oracle's exact candidates: 0/8 when
@@ -716,8 +724,12 @@ def test_c3_int8_pruning_tiers_vs_oracle(az, n, q):
     else the eighths computed before the decision; the tiers-only run (FLACMI_FLAG_TIERS_ONLY)
     takes the eighths for every unit.  Each outcome occurs: pruned by the sign bound, pruned
     after two eighths, pruned later, every eighth then fixed, LPC chosen, a near tie, and
-    (n = 4096) the tie AssertionError (encoder.py:133-157)."""
-    L = 32
+    (n = 4096) the tie AssertionError (encoder.py:133-157).  At n = 16384 production runs
+    k_resid_sb (the bound first over the block's first half, then over all of it; decided units
+    never reach the int8 path, so units outside it can prune too); L = 16 / 20 pin the bound's
+    indexing for the LMAX = 16 and 32 template buckets below L = 32."""
+    lmax = 16 if L <= 16 else 32
+    lean = _sb_lean(n)
     a = _c3_tier_units(n, q)
     nu = len(a)
     ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, 8), n, sample_bits=24, threads=16)
@@ -737,15 +749,17 @@ def test_c3_int8_pruning_tiers_vs_oracle(az, n, q):
         if st != 0 and int(om["site"][u]) != abi.SITE_CHOICE_TIE:
             continue
         tiers = int(tm["lpc_tiers"][u])
+        sbp = _emulate_sign_bound(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u], lmax, lean)
         if not _int8_path(a[u], ora["lpc_records"][u], L):  # the int64 chains: exact, no pruning
             assert tiers == 0 and int(tm["lpc_order"][u]) != abi.LPC_PRUNED, (u, "int64 path", tiers)
-            assert int(pm["lpc_tiers"][u]) == 0 and int(pm["lpc_order"][u]) != abi.LPC_PRUNED, (u, "int64 path")
+            want_p = lean and sbp  # k_resid_sb decides before any int8 check
+            assert int(pm["lpc_tiers"][u]) == ((8 << 8) if want_p else 0), (u, "int64 path", int(pm["lpc_tiers"][u]))
+            assert (int(pm["lpc_order"][u]) == abi.LPC_PRUNED) == want_p, (u, "int64 path")
             seen.add("int64")
             continue
         done, pr = _emulate_eighths(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u])
         assert tiers == done | (8 << 8), (u, "lpc_tiers", tiers & 0xff, tiers >> 8, "want", done)
         assert (int(tm["lpc_order"][u]) == abi.LPC_PRUNED) == pr, (u, "pruned")
-        sbp = _emulate_sign_bound(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u])
         want_prod = (8 << 8) if sbp else done | (8 << 8)
         assert int(pm["lpc_tiers"][u]) == want_prod, (u, "production lpc_tiers", int(pm["lpc_tiers"][u]), want_prod)
         assert (int(pm["lpc_order"][u]) == abi.LPC_PRUNED) == (sbp or pr), (u, "pruned (production)")
@@ -762,5 +776,50 @@ def test_c3_int8_pruning_tiers_vs_oracle(az, n, q):
             seen.add("exact-fixed")
         if st == 0 and not pr and abs(int(om["lpc_sum"][u]) - int(om["fixed_sum"][u])) <= 1e-3 * int(om["fixed_sum"][u]):
             seen.add("near-tie")
-    want = {"sign-bound", "pruned@2", "pruned-later", "exact-fixed", "lpc", "near-tie"} | ({"tie"} if n == 4096 else set())
+    if L == 32:
+        want = {"sign-bound", "pruned@2", "pruned-later", "exact-fixed", "lpc", "near-tie"} | ({"tie"} if n == 4096 else set())
+    else:
+        want = {"sign-bound", "pruned@2", "exact-fixed"}
     assert want <= seen, want - seen
+
+
+def test_mf8_persistent_grid_loops_over_units(az, monkeypatch):
+    """kVarMf8's persistent grid (k_resid.h) with every workgroup looping over many units:
+    FLACMI_MF8_GRID=4 caps it (and the 64-bit list variant's grid) at four workgroups, so the
+    next unit's LDS-DMA copy, the raw barriers and the next unit's record status and words
+    carried in registers all run (the uncapped grid has a workgroup per unit for test-sized
+    batches).  The batch mixes pruned units, units that run every eighth, LPC
+    winners, a unit whose LPC record carries an exception (a silent block), units outside the
+    int8 path (a top digit of 128: listed for kVarList1), and a short run of each kind between
+    them.  Tiers-only runs (kVarMf8), then production runs (k_resid_sb + kVarList1), capped vs
+    uncapped vs the oracle, every meta field (lpc_tiers included), parameter and residual."""
+    n, L, q = 16384, 32, 15
+    base = _c3_tier_units(n, q)
+    odd = oracle.synth_batch(900, 6, n, 24, 5, dtype=np.int32)
+    odd[0, 4000] = 8355712   # top digit 128: the int64 chains (listed)
+    odd[1, :] = 0            # a silent block: the LPC record's exception
+    odd[2, 100:] = 0
+    odd[3, 77] = 2 ** 23 - 1  # above 8355711 too
+    a = np.ascontiguousarray(np.concatenate([base[:20], odd, base[20:], odd[[0, 3]], base[:10]]))
+    nu = len(a)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, 8), n, sample_bits=24, threads=16)
+    runs = {}
+    for cap in ("", "4", "3"):
+        if cap:
+            monkeypatch.setenv("FLACMI_MF8_GRID", cap)
+        else:
+            monkeypatch.delenv("FLACMI_MF8_GRID", raising=False)
+        for kind in ("tier", "prod"):
+            p = make_params(L, q, 0, 8, tiers_only=(kind == "tier"))
+            runs[(cap, kind)] = az.analyze(a, p, n, sample_bits=24)
+    monkeypatch.delenv("FLACMI_MF8_GRID", raising=False)
+    for (cap, kind), out in runs.items():
+        compare_with_oracle(out, ora, [n] * nu)
+        ref = runs[("", kind)]
+        for f in abi.META_DTYPE.names:
+            assert np.array_equal(out["meta"][f], ref["meta"][f]), (cap, kind, f)
+        assert np.array_equal(out["residual"], ref["residual"]), (cap, kind)
+        assert np.array_equal(out["rice_params"], ref["rice_params"]), (cap, kind)
+    tm, om = runs[("4", "tier")]["meta"], ora["meta"]
+    assert (om["status"] != 0).any() and (om["kind"] == abi.KIND_LPC).any()
+    assert (tm["lpc_order"] == abi.LPC_PRUNED).any() and ((tm["lpc_tiers"] & 0xff) == 8).any()

@@ -39,10 +39,11 @@ def test_sign_bound_is_a_lower_bound(n, bits, L, q):
         if int(ora["meta"]["status"][u]) != 0 or int(ora["lpc_records"][u][0]) != 0:
             continue
         rec, fs, ls = ora["lpc_records"][u], ora["fixed_sums"][u], ora["lpc_sums"][u]
-        for p, lb in enumerate(sign_bound.order_bounds(a[u], rec, L), start=1):
-            if lb is not None:
-                assert lb <= int(ls[p - 1]), (u, p, lb, int(ls[p - 1]))
-        if sign_bound.decides(a[u], rec, L, fs):
+        for hi in (None, n // 2, 4096):  # the whole R, and k_resid_sb's first tests ([lmax, hi))
+            for p, lb in enumerate(sign_bound.order_bounds(a[u], rec, L, hi=hi), start=1):
+                if lb is not None:
+                    assert lb <= int(ls[p - 1]), (u, p, hi, lb, int(ls[p - 1]))
+        if sign_bound.decides(a[u], rec, L, fs, split_end=n // 2):
             decided += 1
             assert int(ora["meta"]["lpc_sum"][u]) > int(ora["meta"]["fixed_sum"][u]), u
     assert decided > 0
