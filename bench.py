@@ -379,18 +379,25 @@ def all_ranks_ok(ok, dist, device=None):
 def open_stats_comm(az, dist, rank, world, device):
     """The C-ABI stats communicator of an N-rank job: rank 0's id broadcast over the process
     group, then flacmi_comm_init on every rank (a collective call).  -> (comm, reason): comm
-    None, with the reason, when some rank cannot load RCCL or build the communicator (every
-    rank first asks for an id, which loads RCCL, and all agree before the collective init),
-    so the job reduces through torch.distributed instead of failing."""
+    None, with the reason, when some rank cannot load RCCL or build the communicator, so the
+    job reduces through torch.distributed instead of failing.  Every rank's local
+    preconditions run first and all ranks agree on them before the collective init: the
+    device is set when the Analyzer opens its context, flacmi_comm_available loads RCCL and
+    its entry points (no id, no listener), and only rank 0 calls flacmi_comm_id (an id makes a
+    bootstrap listener).  Not covered: a rank failing inside ncclCommInitRank itself, after
+    the others have entered it (they then block in RCCL's bootstrap)."""
     from flac_amd import abi
     from flac_amd.analysis import StatsComm
-    why = ""
+    why, cid = "", None
     try:
-        cid = StatsComm.comm_id(az.lib)  # every rank: proves RCCL loads here; rank 0's is used
+        StatsComm.available(az.lib)
+        if rank == 0:
+            cid = StatsComm.comm_id(az.lib)
+        ok = True
     except Exception as e:  # noqa: BLE001 (recorded in the bench line)
-        cid, why = None, f"rank {rank}: flacmi_comm_id: {e}"
-    if not all_ranks_ok(cid is not None, dist, device):
-        return None, why or "a rank could not load RCCL (flacmi_comm_id)"
+        ok, why = False, f"rank {rank}: {'flacmi_comm_id' if 'comm_id' in str(e) else 'flacmi_comm_available'}: {e}"
+    if not all_ranks_ok(ok, dist, device):
+        return None, why or "a rank could not load RCCL (flacmi_comm_available / flacmi_comm_id)"
     cid = broadcast_comm_id(cid if rank == 0 else None, dist, abi.COMM_ID_BYTES, device)
     comm = None
     try:

@@ -376,6 +376,12 @@ class StatsComm:
         self.comm = h.value
 
     @staticmethod
+    def available(lib) -> None:
+        """Raises FlacmiError unless RCCL loads here (no id made: the check every rank runs
+        before rank 0's comm_id and the collective init)."""
+        check(lib.flacmi_comm_available(), "flacmi_comm_available")
+
+    @staticmethod
     def comm_id(lib) -> bytes:
         buf = C.create_string_buffer(abi.COMM_ID_BYTES)
         check(lib.flacmi_comm_id(buf), "flacmi_comm_id")

@@ -116,9 +116,15 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-/* |a - b| + c on biased (x ^ 0x80000000) operands: one v_sad_u32. */
+/* |a - b| + c on biased (x ^ 0x80000000) operands: one v_sad_u32 (the compiler's own
+ * pattern match often misses it and emits min, max, sub and add). */
 __device__ __forceinline__ uint32_t sad_acc(uint32_t a, uint32_t b, uint32_t c) {
     return (a > b ? a - b : b - a) + c;
+}
+/* v_sad_u32 acc + |a - b| as one instruction, forced (the pattern match is lost on a constant b) */
+__device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t acc) {
+    asm("v_sad_u32 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+    return acc;
 }
 constexpr uint32_t kBias = 0x80000000u;
 

@@ -1289,6 +1289,8 @@ struct flacmi_comm {
     int nranks, rank;
 };
 
+int flacmi_comm_available(void) { return rccl_load(); }
+
 int flacmi_comm_id(void* id_out) {
     if (!id_out) return fail(FLACMI_E_INVALID, "null argument");
     if (int rc = rccl_load()) return rc;

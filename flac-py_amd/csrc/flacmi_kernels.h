@@ -62,7 +62,6 @@ struct ResidArgs {
     int32_t persist;                 /* k_resid kVarMf8: the grid loops over the batch and copies the next
                                         unit's samples into LDS (LDS-DMA) during this unit's Rice phase */
     int32_t sign_bound;              /* int8-MFMA pruning: try the sign-correlation bound before the tiers */
-    int32_t sb_split;                /* k_resid_sb: chunks per thread in the bound's first test (0: all) */
 };
 /* internal unit status between the fast and the generic k_resid (never returned) */
 #define FLACMI_STATUS_RETRY 0x7e

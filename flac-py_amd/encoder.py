@@ -333,9 +333,19 @@ class _Session:
                 raise
             return data.tobytes(), offsets, status
 
+    def close(self) -> None:
+        self.pool.shutdown(wait=True)
+        self.stage = [None, None]
+        self.out = None
+        self.az.close()
+
 
 _IDLE = collections.defaultdict(list)   # device -> sessions no running encode holds
 _IDLE_LOCK = threading.Lock()
+# idle sessions kept per device: a burst of concurrent or interleaved generators creates one
+# session each, and each holds a context, pinned staging and frame buffers and a worker
+# thread, so the sessions beyond this many are closed when they come back
+_IDLE_MAX = 2
 
 
 def _sessions(device: int, devices: Optional[Sequence[int]]):
@@ -360,9 +370,13 @@ def _sessions(device: int, devices: Optional[Sequence[int]]):
 
 
 def _release(sessions) -> None:
+    extra = []
     with _IDLE_LOCK:
         for s in sessions:
-            _IDLE[s.az.device].append(s)
+            pool = _IDLE[s.az.device]
+            (pool if len(pool) < _IDLE_MAX else extra).append(s)
+    for s in extra:
+        s.close()
 
 
 def _drive(batches, sessions, params, n, channels, sample_size) -> Iterator[bytes]:

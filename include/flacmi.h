@@ -393,6 +393,10 @@ int flacmi_stream_stats(flacmi_ctx* ctx, const flacmi_unit_meta* d_meta, int64_t
  * the streams' statistics are the only cross-GPU exchange (encoder.py:81 writes no MD5). */
 #define FLACMI_COMM_ID_BYTES 128
 typedef struct flacmi_comm flacmi_comm;
+/* 0 when RCCL loads here with every entry point the communicator uses (a local check, no id
+ * or socket made): every rank runs it before rank 0 makes the id and all ranks enter the
+ * collective flacmi_comm_init.  A failure inside ncclCommInitRank itself is not covered. */
+int flacmi_comm_available(void);
 int flacmi_comm_id(void* id_out);
 int flacmi_comm_init(flacmi_ctx* ctx, int nranks, int rank, const void* id, flacmi_comm** out);
 /* Sum of every rank's FLACMI_STATS_WORDS int64 words, in place (device pointer), enqueued

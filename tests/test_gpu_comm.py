@@ -17,6 +17,7 @@ def test_comm_world_one_allreduce_is_identity():
     from flac_amd.analysis import Analyzer, StatsComm
 
     az = Analyzer(0)
+    StatsComm.available(az.lib)  # RCCL loads (the check every rank runs before the id)
     cid = StatsComm.comm_id(az.lib)
     assert len(cid) == abi.COMM_ID_BYTES
     with pytest.raises(FlacmiError):

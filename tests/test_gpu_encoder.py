@@ -203,3 +203,10 @@ def test_interleaved_generators_do_not_share_staging(enc):
     next(g), next(g), next(g), next(g)
     g.close()
     assert list(enc.encode_planar(44100, 16, a, p, blocks_per_batch=1)) == seq_a
+    # a burst of four concurrent generators: the sessions beyond _IDLE_MAX per device are
+    # closed when they come back (each holds a context, pinned buffers and a worker thread)
+    with concurrent.futures.ThreadPoolExecutor(4) as ex:
+        fs = [ex.submit(lambda: list(enc.encode_planar(44100, 16, a, p, blocks_per_batch=1))) for _ in range(4)]
+        assert all(f.result() == seq_a for f in fs)
+    assert len(enc._IDLE[0]) <= enc._IDLE_MAX
+    assert list(enc.encode_planar(44100, 16, b, p, blocks_per_batch=1)) == seq_b

@@ -667,7 +667,7 @@ def _emulate_eighths(x, rec, L, fixed_sums):
 
 def _sb_lean(n, rmax=8):
     """k_resid.h launch_resid_sb's shapes (k_resid_sb, which tests the bound first over each
-    thread's first chunk: R' = [lmax, 4096) with 512 threads)."""
+    thread's first two chunks: R' = [lmax, 8192) with 512 threads)."""
     om = max(o for o in range(0, rmax + 1) if n % (1 << o) == 0)
     cpp = (n >> om) // 8
     return 8192 <= n <= 16384 and n % 256 == 0 and 6 <= om <= 8 and (n >> om) % 8 == 0 and cpp & (cpp - 1) == 0
@@ -676,7 +676,7 @@ def _sb_lean(n, rmax=8):
 def _emulate_sign_bound(x, rec, L, fixed_sums, lmax=32, lean=False):
     """The sign-correlation bound of mf8_candidate_sums / k_resid_sb restated on the oracle's
     record (tests/sign_bound.py) -> True when every order loses to the best fixed sum."""
-    return sign_bound.decides(x, rec, L, fixed_sums, lmax, split_end=8 * 1 * 512 if lean else None)
+    return sign_bound.decides(x, rec, L, fixed_sums, lmax, split_end=8 * 2 * 512 if lean else None)
 
 
 def _c3_tier_units(n, q):

@@ -160,11 +160,16 @@ def _comm_worker(rank, world, port, out):
     sys.path.insert(0, REPO)
     import bench
 
-    class _NoRccl:  # an analyzer whose library cannot hand out an RCCL id on this rank
+    class _NoRccl:  # an analyzer whose library cannot load RCCL on rank 1
         class lib:  # noqa: N801
             @staticmethod
-            def flacmi_comm_id(buf):
+            def flacmi_comm_available():
                 return -5 if rank == 1 else 0
+
+            @staticmethod
+            def flacmi_comm_id(buf):
+                assert rank == 0, "only rank 0 makes the id"
+                return 0
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
@@ -175,7 +180,7 @@ def _comm_worker(rank, world, port, out):
 
 
 def test_open_stats_comm_falls_back_together():
-    """When one rank cannot load RCCL (flacmi_comm_id fails there), every rank learns it
+    """When one rank cannot load RCCL (flacmi_comm_available fails there), every rank learns it
     before the collective flacmi_comm_init and returns no communicator, so the N-rank bench
     reduces through torch.distributed instead of hanging or failing (the reason goes into
     the bench line's config.stats_collective)."""
@@ -191,5 +196,5 @@ def test_open_stats_comm_falls_back_together():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(none for _, none, _ in res)
-    assert "rank 1" in res[1][2] and "flacmi_comm_id" in res[1][2]
+    assert "rank 1" in res[1][2] and "flacmi_comm_available" in res[1][2]
     assert res[0][2]  # rank 0 reports why too

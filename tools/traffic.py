@@ -31,7 +31,7 @@ def short(name):
 
 
 def stage(name):
-    if short(name).startswith("k_resid_stream"):  # the one-workgroup-per-unit k_resid variant
+    if short(name).startswith(("k_resid_stream", "k_resid_sb")):  # k_resid's one-workgroup-per-unit variants
         return "k_resid"
     for k in STAGES:
         if re.match(k + r"\b", short(name)):
