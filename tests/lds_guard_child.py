@@ -33,10 +33,22 @@ def unit_sets():
     s24 = oracle.synth_batch(0, 20, 2048, 24, 32, dtype=np.int32)
     s24[3, 100:] = 0
     s1k = oracle.synth_batch(0, 24, 1024, 16, 33, dtype=np.int16)
+    # 16384 x 24-bit at L = 32 (config 3's shape): k_resid_sb decides the synthetic units, the
+    # AR(1) and white-noise units go on to kVarList1 (planes and tiers), a top digit of 128
+    # takes the int64 chains there, a silent block carries the LPC record's exception (the
+    # round-4 fault was on the lazy plane build of this family)
+    n3 = 16384
+    s3 = oracle.synth_batch(0, 6, n3, 24, 34, dtype=np.int32)
+    w3 = rng.normal(0, 2e5, (4, n3))
+    w3[:2, 1:] += 0.9 * w3[:2, :-1]
+    s3 = np.concatenate([s3, np.clip(np.round(w3), -2 ** 23, 2 ** 23 - 1).astype(np.int32)])
+    s3[1, 5000] = 8355712
+    s3[2, :] = 0
     return [
         ("s16", s16, n, 16, [(12, 5, 0, 5), (12, 9, 0, 5), (12, 5, 0, 6), (8, 5, 0, 5), (0, 5, 0, 5)]),
         ("s24", s24, 2048, 24, [(32, 15, 0, 6), (16, 12, 0, 5)]),
         ("s1k", s1k, 1024, 16, [(12, 5, 0, 4), (12, 5, 0, 6)]),
+        ("s24k", s3, n3, 24, [(32, 15, 0, 8)]),
     ]
 
 
