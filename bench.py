@@ -338,6 +338,16 @@ def frame_writer_leg(args, cfg, az, samples, meta, rparams, residual, pstride, u
     return res
 
 
+def library_sha16():
+    """sha256[:16] of the libflacmi.so this process loads (flac_amd._lib.LIB_PATH)."""
+    import hashlib
+    from flac_amd import _lib
+    try:
+        return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def shard_first_unit(rank, units_per_rank):
     """First global unit of a rank's shard: contiguous, disjoint block ranges (units are
     independent), so the stream statistics are a plain sum over ranks."""
@@ -643,13 +653,21 @@ def main(argv=None):
     dom_gbs = resid_gbs if dominant == "k_resid" else lpc_gbs
     dom_bytes = resid_b if dominant == "k_resid" else lpc_b
     dom_ms = kt["resid_ms"] if dominant == "k_resid" else kt["lpc_ms"]
-    traffic = None
+    traffic, traffic_lib = None, None
     tfile = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tfile):  # HBM bytes per launch from the separate rocprofv3 --pmc passes
         try:
-            traffic = json.load(open(tfile)).get(dominant)
+            tj = json.load(open(tfile))
+            traffic, traffic_lib = tj.get(dominant), tj.get("library_sha16")
         except Exception:
             traffic = None
+    # counters cannot be collected inside the timed run: the committed figure is current only
+    # while it was measured on this very library
+    lib_now = library_sha16()
+    traffic_current = traffic is not None and traffic_lib is not None and traffic_lib == lib_now
+    if traffic is not None and not traffic_current and rank == 0:
+        print(f"bench.py: {os.path.relpath(tfile, REPO)} was profiled on library {traffic_lib}, this run uses "
+              f"{lib_now}: re-run tools/profile.sh for a current traffic figure", file=sys.stderr)
 
     if rank == 0:
         # rank 0 only, after the timed region (the other ranks are idle by then)
@@ -677,6 +695,8 @@ def main(argv=None):
                          "unit": "GB/s", "frac": dom_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": (os.path.relpath(tfile, REPO) + ": rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                                             "of this config (tools/profile.sh, tools/traffic.py)") if traffic else None,
+                         "traffic_current": traffic_current,  # profiled on the library this run timed
+                         "traffic_library_sha16": traffic_lib, "library_sha16": lib_now,
                          "algorithmic_bytes_per_launch": dom_bytes,
                          "algorithmic_bytes_source": "SURVEY §8d: n*s_in + 4*(n - order) + 16 + 4*2^rmax + 4*L per unit",
                          "kernel_ms": dom_ms,

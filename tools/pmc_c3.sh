@@ -1,4 +1,4 @@
-# SQ counters of the c3 kernels (int8-MFMA k_resid, k_lpc<32>) at 40k units
+# SQ counters of the c3 kernels (k_resid_sb, the int8-MFMA k_resid variants, k_lpc<32>) at 40k units
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-pmc_c3}
@@ -11,4 +11,4 @@ for P in "$P1" "$P2"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- python3 bench.py $ARGS > $OUT/p$i.json 2> $OUT/p$i.err || { echo "pass $i failed"; tail -5 $OUT/p$i.err; exit 1; }
 done
-python3 tools/pmc_summary.py $OUT > $OUT/summary.txt && grep -A18 "k_resid<32" $OUT/summary.txt | head -20
+python3 tools/pmc_summary.py $OUT > $OUT/summary.txt && grep -A18 "k_resid" $OUT/summary.txt | head -60

@@ -39,8 +39,19 @@ def stage(name):
     return None
 
 
+def lib_sha16(path=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "flac-py_amd",
+                                  "libflacmi.so")):
+    """sha256[:16] of the library the profile timed (bench.py flags a traffic file whose
+    library differs from the one it runs)."""
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def main(d):
-    res = {"kernels": {}}
+    res = {"kernels": {}, "library_sha16": lib_sha16()}
     for r in rows(os.path.join(d, "trace", "**", "*kernel_stats.csv")):
         res["kernels"].setdefault(short(r["Name"]), {})["avg_ms"] = float(r["AverageNs"]) / 1e6
     for counter, scale in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 1.0)):
