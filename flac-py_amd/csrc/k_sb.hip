@@ -28,6 +28,7 @@ namespace flacmi {
  *      (no LDS copy of it), the meta record and the parameters.
  * ======================================================================================= */
 constexpr int kSbThreads = 512;
+constexpr int kSbChunks = 4; /* 8-sample chunks per thread at n <= 16384 */
 constexpr int kSbSplit = 2; /* chunks per thread in the bound's first pass; the second pass takes
                              * the rest (<= 2 at n <= 16384): <= 16 terms per lane and pass */
 struct SbLds {
@@ -334,18 +335,39 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
     auto tail = [&](auto K_) __attribute__((always_inline)) {
         constexpr int K = decltype(K_)::value;
         uint32_t* __restrict__ rout = reinterpret_cast<uint32_t*>(a.residual) + gid * a.residual_stride;
-#pragma unroll 1
-        for (int c = tid; c < nch; c += NT) {
-            uint32_t zv[8];
-            fixed_resid_chunk32<K>(xs, 8 * c, n, zv);
-            reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{zv[0], zv[1], zv[2], zv[3]};
-            reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{zv[4], zv[5], zv[6], zv[7]};
-            uint32_t c32 = 0; /* every value < 2^28: eight < 2^31 */
+        /* the residual stays in registers for the data-bits pass (kept, not recomputed): at most
+         * kSbChunks chunks per thread (n <= 16384) */
+        uint32_t zr[kSbChunks][8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) c32 += zv[k];
-            uint64_t cs8 = c32;
-            for (int w = 1; w < cpp; w <<= 1) cs8 += (uint64_t)__shfl_xor((unsigned long long)cs8, w);
-            if ((c & (cpp - 1)) == 0) fs[P + c / cpp] = cs8;
+        for (int j = 0; j < kSbChunks; ++j) {
+            const int c = tid + j * NT;
+            if (c < nch) { /* whole 32-lane groups: nch % 32 == 0 and the partitions' chunk runs divide 32 */
+                fixed_resid_chunk32<K>(xs, 8 * c, n, zr[j]);
+                reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{zr[j][0], zr[j][1], zr[j][2], zr[j][3]};
+                reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{zr[j][4], zr[j][5], zr[j][6], zr[j][7]};
+                uint32_t c32 = 0; /* every value < 2^28: eight < 2^31 */
+#pragma unroll
+                for (int k = 0; k < 8; ++k) c32 += zr[j][k];
+                /* the finest partition's sum over its cpp consecutive lanes: DPP steps in 32 bits
+                 * while every chunk sum of the wave is < 2^26 (a partition of <= 32 chunks then
+                 * stays < 2^31), else 64-bit shuffles */
+                uint64_t cs8;
+                if (__ballot(c32 >= (1u << 26)) == 0 && cpp <= 16) {
+                    uint32_t v = c32;
+                    if (cpp >= 2) v += dpp_u32<0xB1, 0xf>(v);  /* quad_perm [1,0,3,2] */
+                    if (cpp >= 4) v += dpp_u32<0x4E, 0xf>(v);  /* quad_perm [2,3,0,1] */
+                    if (cpp >= 8) v += dpp_u32<0x141, 0xf>(v); /* row_half_mirror: the other quad */
+                    if (cpp >= 16) v += dpp_u32<0x140, 0xf>(v); /* row_mirror: the other half row */
+                    cs8 = v;
+                } else {
+                    cs8 = c32;
+                    for (int w = 1; w < cpp; w <<= 1) cs8 += (uint64_t)__shfl_xor((unsigned long long)cs8, w);
+                }
+                if ((c & (cpp - 1)) == 0) fs[P + c / cpp] = cs8;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) zr[j][k] = 0;
+            }
         }
         __syncthreads();
         if (a.stop_after == 4) return;
@@ -436,17 +458,18 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
         }
         __syncthreads();
         if (a.stop_after == 6) return;
-        /* data bits: sum over the residual (recomputed from the samples) of (z >> p) for every
-         * candidate order; y = z >> pm as packed 16-bit pairs where it fits */
+        /* data bits: sum over the residual (the registers of the residual pass) of (z >> p) for
+         * every candidate order; y = z >> pm as packed 16-bit pairs where it fits */
         const uint4* pkv = reinterpret_cast<const uint4*>(pk);
         uint64_t tb[16];
         uint32_t tp[16]; /* packed-path totals: < 4 chunks * 8 * 2^16 per order */
 #pragma unroll
         for (int o = 0; o < 16; ++o) tb[o] = 0, tp[o] = 0;
-#pragma unroll 1
-        for (int c = tid; c < nch; c += NT) {
-            uint32_t z[8];
-            fixed_resid_chunk32<K>(xs, 8 * c, n, z);
+#pragma unroll
+        for (int j = 0; j < kSbChunks; ++j) {
+            const int c = tid + j * NT;
+            if (c >= nch) continue;
+            const uint32_t(&z)[8] = zr[j];
             const uint4 pv = pkv[c / cpp];
             const uint32_t pm = pv.w >> 24;
             uint32_t y[8], yo = 0;
