@@ -190,11 +190,11 @@ def end_to_end_leg(args, cfg, az):
     import numpy as np
     import torch
 
-    from flac_amd.analysis import make_params
+    from flac_amd.analysis import make_params, unit_stride
     n, bits, C = cfg["n"], cfg["bits"], cfg["channels"]
     units = (args.e2e_units // C) * C
     dt = torch.int16 if bits <= 16 else torch.int32
-    stride = ((n * (2 if bits <= 16 else 4) + 15) // 16) * 16 // (2 if bits <= 16 else 4)
+    stride = unit_stride(n, 2 if bits <= 16 else 4)
     dev = torch.device("cuda", torch.cuda.current_device())
     g = torch.empty((units, stride), dtype=dt, device=dev)
     az.synth_device(g.data_ptr(), g.element_size(), bits, stride, 10_000_000, units, n, args.seed)
@@ -533,7 +533,7 @@ def main(argv=None):
     torch.cuda.set_device(dev)
 
     from flac_amd import abi
-    from flac_amd.analysis import Analyzer, make_params, params_stride_for
+    from flac_amd.analysis import Analyzer, make_params, params_stride_for, unit_stride
 
     az = Analyzer(local)
     stream = torch.cuda.current_stream(dev)
@@ -541,7 +541,7 @@ def main(argv=None):
     n, bits = cfg["n"], cfg["bits"]
     sdt = torch.int16 if bits <= 16 else torch.int32
     sbytes = 2 if bits <= 16 else 4
-    sstride = ((n * sbytes + 15) // 16) * 16 // sbytes
+    sstride = unit_stride(n, sbytes)
     rstride = ((n * 4 + 15) // 16) * 16 // 4
     pstride = params_stride_for(cfg["rmax"])
     first_unit, my_chunks, total_units = shard_plan(cfg, rank, world, units, args.total_units)

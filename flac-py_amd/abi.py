@@ -228,6 +228,7 @@ SIGNATURES = {
     "flacmi_stream_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
                                       C.c_int64, C.c_void_p, C.c_void_p]),
     "flacmi_comm_available": (C.c_int, []),
+    "flacmi_unit_stride": (C.c_int64, [C.c_int32, C.c_int32]),
     "flacmi_comm_id": (C.c_int, [C.c_void_p]),
     "flacmi_comm_init": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
     "flacmi_allreduce_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),

@@ -55,6 +55,14 @@ def device_batch(samples_ptr: int, sample_bytes: int, sample_bits: int, unit_str
     return b
 
 
+def unit_stride(block_len: int, sample_bytes: int) -> int:
+    """The row pitch (samples) the library lays device rows out at (flacmi_unit_stride): 16-byte
+    rows, plus 128 bytes when the pitch is a multiple of 4 KB."""
+    v = load().flacmi_unit_stride(block_len, sample_bytes)
+    check(v if v < 0 else 0, "flacmi_unit_stride")
+    return v
+
+
 def params_stride_for(rice_max: int) -> int:
     return (1 << max(rice_max, 0)) + 1
 

@@ -187,6 +187,13 @@ static int ensure_buf(DevBuf& b, size_t bytes) {
     return 0;
 }
 
+/* device row pitch in samples (flacmi_unit_stride) */
+static int64_t row_pitch(int64_t n, int64_t sample_bytes) {
+    int64_t bytes = ((n * sample_bytes + 15) / 16) * 16;
+    if (bytes % 4096 == 0) bytes += 128;
+    return bytes / sample_bytes;
+}
+
 static int set_device(flacmi_ctx* ctx) {
     if (!ctx) return fail(FLACMI_E_INVALID, "null context");
     HIP_TRY(hipSetDevice(ctx->device));
@@ -605,7 +612,7 @@ int flacmi_analyze_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi
     if (int rc = set_device(ctx)) return rc;
     const size_t nu = (size_t)batch->n_units;
     /* device mirrors with 16-byte aligned rows */
-    const int64_t sstride = ((batch->block_len * batch->sample_bytes + 15) / 16) * 16 / batch->sample_bytes;
+    const int64_t sstride = row_pitch(batch->block_len, batch->sample_bytes);
     const int64_t rstride = ((batch->block_len * out->residual_bytes + 15) / 16) * 16 / out->residual_bytes;
     if (int rc = ensure_buf(ctx->h_samples, nu * sstride * batch->sample_bytes)) return rc;
     if (int rc = ensure_buf(ctx->h_meta, nu * sizeof(flacmi_unit_meta))) return rc;
@@ -827,7 +834,7 @@ int flacmi_encode_host(flacmi_ctx* ctx, const flacmi_batch* batch, const flacmi_
     }
     if (int rc = set_device(ctx)) return rc;
     const size_t nu = (size_t)batch->n_units;
-    const int64_t sstride = ((batch->block_len * batch->sample_bytes + 15) / 16) * 16 / batch->sample_bytes;
+    const int64_t sstride = row_pitch(batch->block_len, batch->sample_bytes);
     const int64_t pstride = (1LL << (params->rice_max > 0 ? params->rice_max : 0)) + 1;
     if (int rc = ensure_buf(ctx->h_samples, nu * sstride * batch->sample_bytes)) return rc;
     if (int rc = ensure_buf(ctx->h_meta, nu * sizeof(flacmi_unit_meta))) return rc;
@@ -980,7 +987,7 @@ static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, co
     const size_t nu = (size_t)b.n_units;
     /* rows already at the padded device stride go as one linear copy; any other stride (a
        row view of a wider array) is packed to padded device rows by a 2-D copy */
-    const int64_t padded = ((b.block_len * b.sample_bytes + 15) / 16) * 16 / b.sample_bytes;
+    const int64_t padded = row_pitch(b.block_len, b.sample_bytes);
     const bool linear = whole->unit_stride == padded;
     sl.dstride = padded;
     const int64_t sstride = sl.dstride;
@@ -1290,6 +1297,11 @@ struct flacmi_comm {
 };
 
 int flacmi_comm_available(void) { return rccl_load(); }
+
+int64_t flacmi_unit_stride(int32_t block_len, int32_t sample_bytes) {
+    if (block_len < 1 || (sample_bytes != 2 && sample_bytes != 4)) return fail(FLACMI_E_INVALID, "block_len < 1 or sample_bytes not 2/4");
+    return row_pitch(block_len, sample_bytes);
+}
 
 int flacmi_comm_id(void* id_out) {
     if (!id_out) return fail(FLACMI_E_INVALID, "null argument");

@@ -208,6 +208,18 @@ __device__ __forceinline__ uint32_t pk_shr_bcast(uint32_t s, uint32_t d) {
     return r;
 }
 
+/* one chunk's eight zig-zag values to the residual row (FLACMI_NT_STORE: non-temporal, A/B) */
+__device__ __forceinline__ void store_row(uint32_t* r, const uint32_t (&z)[8]) {
+#if FLACMI_NT_STORE
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(v4u{z[0], z[1], z[2], z[3]}, reinterpret_cast<v4u*>(r));
+    __builtin_nontemporal_store(v4u{z[4], z[5], z[6], z[7]}, reinterpret_cast<v4u*>(r) + 1);
+#else
+    reinterpret_cast<uint4*>(r)[0] = uint4{z[0], z[1], z[2], z[3]};
+    reinterpret_cast<uint4*>(r)[1] = uint4{z[4], z[5], z[6], z[7]};
+#endif
+}
+
 /* fixed order K residual of samples i0..i0+7 from biased LDS samples, zig-zagged; the
  * warm-up samples (i < K) give 0 */
 template <int K, bool FIRST = true>
@@ -340,7 +352,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
          * inside a guarded block gets its own s_waitcnt there, serialising the HBM trips) */
         uint4 q[kSCPT];
 #pragma unroll
-        for (int j = 0; j < kSCPT; ++j) q[j] = src[min(tid + j * NT, nch - 1)];
+        for (int j = 0; j < kSCPT; ++j) {
+#if FLACMI_NT_LOAD
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(src) + min(tid + j * NT, nch - 1));
+            q[j] = uint4{t.x, t.y, t.z, t.w};
+#else
+            q[j] = src[min(tid + j * NT, nch - 1)];
+#endif
+        }
         fixb = reinterpret_cast<const uint4*>(kFixB.w)[lane];
         /* tap table words tid + j NT: word w of row p holds (T_p[16 - 2w], T_p[15 - 2w]); the
          * record values it needs are loaded here, with the samples (clamped, unconditional) */
@@ -359,7 +379,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             }
         }
         if (tid < kSHP) xs[tid - kSHP] = 0x8000u; /* biased zeros */
-        if (tid < Pmax) pks[tid] = 0;
+        if (tid < Pmax) pks[tid] = a.stop_after == 10 ? (uint32_t)n * 40u : 0u; /* 10: no atomics, sums nonzero */
         const uint32_t k8000 = opaque(0x8000u);
         uint32_t sumx = 0;
 #pragma unroll
@@ -736,6 +756,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                 break;
         }
     };
+    const bool pairs = (cpp & 1) == 0 && a.stop_after != 9;
     uint32_t zp[kSCPT][4]; /* 16-bit pairs of the chunk's residual */
     uint32_t big = 0;     /* bit j: chunk j holds a value >= 2^16 */
     /* one copy of the chunk loop per predictor (the switch is taken once, not per chunk) */
@@ -749,10 +770,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                 uint32_t z[8];
                 if (j == 0) fixed_chunk<KK, true>(xs, 8 * c, z);
                 else fixed_chunk<KK, false>(xs, 8 * c, z);
-                reinterpret_cast<uint4*>(rout + 8 * c)[0] = uint4{z[0], z[1], z[2], z[3]};
-                reinterpret_cast<uint4*>(rout + 8 * c)[1] = uint4{z[4], z[5], z[6], z[7]};
-                const uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
-                if (omax >= 0) atomicAdd(&pks[part_of(c)], cs);
+                store_row(rout + 8 * c, z);
+                uint32_t cs = z[0] + z[1] + z[2] + z[3] + z[4] + z[5] + z[6] + z[7];
+                /* chunks 2m and 2m + 1 (lanes l and l ^ 1) share a finest partition when it
+                 * holds an even number of chunks: one lane adds both, halving the same-address
+                 * LDS atomics (stop_after 9: every lane adds, 10: none; timing only) */
+                if (pairs) cs += dpp_u32<0xB1, 0xf>(cs);
+                if (omax >= 0 && a.stop_after != 10 && (!pairs || (lane & 1) == 0)) atomicAdd(&pks[part_of(c)], cs);
                 if ((z[0] | z[1] | z[2] | z[3] | z[4] | z[5] | z[6] | z[7]) >> 16) big |= 1u << j;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) zp[j][i] = __builtin_amdgcn_perm(z[2 * i + 1], z[2 * i], 0x05040100u);

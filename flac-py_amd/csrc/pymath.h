@@ -172,6 +172,7 @@ PYM_HD double py_pow2(double x, const PowTables& T, int* status) {
 
 /* floor(log2(x)) for finite x > 0.  thr[e + 1074] = smallest double in [2^e, 2^(e+1))
  * whose libm log2 is >= e + 1 (2^(e+1) if none), for e in [-1074, 1023]. */
+#define PYM_LOG2_THR_N 2098 /* e in [-1074, 1023] */
 PYM_HD int py_floor_log2(double x, const double* thr) {
     const uint64_t u = as_u64(x);
     int e = (int)((u >> 52) & 0x7ff);
@@ -181,9 +182,11 @@ PYM_HD int py_floor_log2(double x, const double* thr) {
     } else {
         e -= 1023;
     }
-    return x >= thr[e + 1074] ? e + 1 : e;
+    /* the index is clamped into the table: a caller outside the contract (inf, NaN, 0) gets a
+     * wrong value, never a read past the table */
+    const int ti = e + 1074 < 0 ? 0 : e + 1074 > PYM_LOG2_THR_N - 1 ? PYM_LOG2_THR_N - 1 : e + 1074;
+    return x >= thr[ti] ? e + 1 : e;
 }
 
-#define PYM_LOG2_THR_N 2098 /* e in [-1074, 1023] */
 
 }  // namespace pym

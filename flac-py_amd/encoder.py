@@ -22,7 +22,7 @@ import numpy as np
 from . import abi
 from . import coded_number
 from ._lib import FlacmiError
-from .analysis import Analyzer, make_params, params_stride_for
+from .analysis import Analyzer, make_params, params_stride_for, unit_stride
 from .binary import Put
 from .common import (
     CHANNELS_ENCODING, CRC8_POLYNOMIAL, FRAME_SYNC_CODE, MAGIC,
@@ -120,7 +120,7 @@ def _planar(blocks, channels: int, block_len: int, alloc=None):
         rows[b * channels:(b + 1) * channels, :len(xs)] = a.T
     bits = _sample_bits(rows)
     dt = np.int16 if bits <= 16 else np.int32
-    stride = ((block_len * np.dtype(dt).itemsize + 15) // 16) * 16 // np.dtype(dt).itemsize
+    stride = unit_stride(block_len, np.dtype(dt).itemsize)
     if alloc is None:
         out = np.zeros((nb * channels, stride), dtype=dt)
     else:
@@ -443,7 +443,7 @@ def _one(samples, params, bits=None):
     n = len(xs)
     bits = bits or _sample_bits(xs)
     dt = np.int16 if bits <= 16 else np.int32
-    stride = max(8, ((n * np.dtype(dt).itemsize + 15) // 16) * 16 // np.dtype(dt).itemsize)
+    stride = max(8, unit_stride(n, np.dtype(dt).itemsize))
     row = np.zeros((1, stride), dtype=dt)
     row[0, :n] = xs
     out = _analyzer(0).analyze(row, params, n, sample_bits=bits)

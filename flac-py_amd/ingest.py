@@ -20,6 +20,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
+from .analysis import unit_stride
+
 
 @dataclass
 class PcmInfo:
@@ -121,7 +123,8 @@ def sample_bits(pcm: np.ndarray) -> int:
 def planar_blocks(pcm: np.ndarray, block_size: int, first_block: int = 0, n_blocks: int = -1, alloc=None):
     """int64 [channels][frames] -> (rows [n_blocks*channels][stride] int16/int32, bits,
     tail_len, n_tail_units) for blocks [first_block, first_block + n_blocks) of
-    utils.batch(frames, block_size).  Rows are 16-byte aligned; samples past a short
+    utils.batch(frames, block_size).  Rows are at the library's device pitch
+    (flacmi_unit_stride), so a batch goes to the device as one linear copy; samples past a short
     block's end are zero.  alloc(shape, dtype) (optional) supplies the rows' memory, e.g.
     a page-locked staging buffer reused batch after batch."""
     C, frames = pcm.shape
@@ -135,7 +138,7 @@ def planar_blocks(pcm: np.ndarray, block_size: int, first_block: int = 0, n_bloc
     bits = sample_bits(seg)
     dt = np.int16 if bits <= 16 else np.int32
     isz = np.dtype(dt).itemsize
-    stride = ((block_size * isz + 15) // 16) * 16 // isz
+    stride = unit_stride(block_size, isz)
     if alloc is None:
         rows = np.zeros((n_blocks, C, stride), dtype=dt)
     else:

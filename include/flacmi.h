@@ -148,7 +148,8 @@ typedef struct flacmi_batch {
     const void* samples;     /* int16 (sample_bytes 2) or int32 (sample_bytes 4) */
     int32_t sample_bytes;    /* 2 or 4 */
     int32_t sample_bits;     /* every sample fits a signed integer of this many bits (<= 8*sample_bytes) */
-    int64_t unit_stride;     /* elements between consecutive units */
+    int64_t unit_stride;     /* elements between consecutive units (flacmi_unit_stride: the pitch
+                                the library itself lays rows out at) */
     int64_t n_units;
     int32_t block_len;       /* 1..FLACMI_MAX_BLOCK */
     int32_t tail_len;        /* length of the trailing units, 1..block_len (ignored if n_tail_units == 0) */
@@ -403,6 +404,15 @@ int flacmi_comm_init(flacmi_ctx* ctx, int nranks, int rank, const void* id, flac
  * on `stream` (a stream of the communicator's context device). */
 int flacmi_allreduce_stats(flacmi_comm* comm, int64_t* d_stats, void* stream);
 int flacmi_comm_destroy(flacmi_comm* comm);
+
+/* ---- row layout ------------------------------------------------------------------------ */
+/* The unit pitch, in samples, at which this library lays out device rows (the *_host entry
+ * points' mirrors, the encode pipeline's sub-batches) and which it recommends to callers of
+ * the *_device entry points: the row rounded up to 16 bytes, plus 128 bytes when that is a
+ * multiple of 4 KB.  k_lpc reads 64 rows at one offset per load instruction; at a 4 KB-multiple
+ * pitch those lines fall into the same L2 sets and are fetched again.  A host
+ * batch already at this pitch goes to the device as one linear copy.  No device needed. */
+int64_t flacmi_unit_stride(int32_t block_len, int32_t sample_bytes);
 
 /* ---- synthetic PCM (BASELINE configs 2-5) --------------------------------- */
 /* Writes units [first_unit, first_unit + n_units) of the integer synthetic signal into

@@ -55,6 +55,24 @@ def test_struct_layouts_match_header(tmp_path):
     assert abi.META_DTYPE.itemsize == ctypes.sizeof(abi.UnitMeta)
 
 
+def test_unit_stride_pads_4k_multiple_rows():
+    """flacmi_unit_stride: 16-byte rows, plus 128 bytes when the pitch is a multiple of 4 KB
+    (config 3's 16384 x int32 rows: k_lpc FETCH 1.72x -> 1.03x of the sample bytes)."""
+    from flac_amd.analysis import unit_stride
+    lib = load()
+    assert unit_stride(4608, 2) == 4608          # config 2: 9216-byte rows, unpadded
+    assert unit_stride(1152, 2) == 1152
+    assert unit_stride(4097, 2) == 4104          # rounded up to 16 bytes
+    assert unit_stride(16384, 4) == 16384 + 32   # config 3
+    assert unit_stride(4096, 2) == 4096 + 64
+    assert unit_stride(2048, 4) == 2048 + 32
+    for n in range(1, 5000, 7):
+        for b in (2, 4):
+            v = unit_stride(n, b)
+            assert v >= n and (v * b) % 16 == 0 and (v * b) % 4096 != 0
+    assert lib.flacmi_unit_stride(0, 2) < 0 and lib.flacmi_unit_stride(16, 3) < 0
+
+
 def test_create_without_device_fails_loudly():
     lib = load()
     if lib.flacmi_device_count() > 0:
