@@ -254,7 +254,8 @@ __host__ __device__ inline ResidLds resid_lds_layout(int lmax, int n, int nw, in
     o = o > pl_end ? o : pl_end;
     l.coef = o; o = up(o + coef_bytes);
     /* the int8-MFMA path's pruning tiers alternate between two copies (one barrier per test) */
-    l.red = o;  o = up(o + 8 * nw * (nsum > 16 ? nsum : 16) * (planes ? 2 : 1));
+    /* (nsum + 1 per wave: the 16-bit sign bound's fixed sums and K_0 .. K_lmax) */
+    l.red = o;  o = up(o + 8 * nw * (nsum + 1 > 16 ? nsum + 1 : 16) * (planes ? 2 : 1));
     l.dec = o;  o = up(o + (int)sizeof(Decision));
     l.rb = o;   o = up(o + 8 * 32);
     l.misc = o; o = up(o + 4 * 8);

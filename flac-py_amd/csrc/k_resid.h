@@ -132,6 +132,30 @@ struct CoefTables {
 };
 constexpr int kTapW = 20;
 
+/* The sign-correlation bound's terms over one chunk of 16-bit samples (window at i0 >= HP):
+ * K_j += sum_i w_i x_{i-j} for j = 0..LMAX with w_i = sign(x_i) as packed +-1 halves, one
+ * v_dot2_i32_i16 per sample pair and lag (exact: no N_- correction inside K_j), and
+ * nneg += #{x_i < 0} (the bound's -N_- term). */
+template <int LMAX, int HP>
+__device__ __forceinline__ void sb16_chunk(const Win16<HP>& W, int32_t (&kk)[LMAX + 1], uint32_t& nneg) {
+    static_assert(HP % 2 == 0 && HP >= LMAX, "window pairs start at even positions and cover every lag");
+    const uint32_t k15 = 0x000F000Fu;
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {
+        const uint32_t xp = W.E[(HP + k) >> 1]; /* samples i0 + k (lo), i0 + k + 1 (hi) */
+        uint32_t sg;
+        asm("v_pk_ashrrev_i16 %0, %1, %2" : "=v"(sg) : "v"(k15), "v"(xp));
+        sg |= 0x00010001u; /* +1 or -1 per half */
+        nneg += (uint32_t)__builtin_popcount(xp & 0x80008000u);
+#pragma unroll
+        for (int j = 0; j <= LMAX; ++j) {
+            const int lo = HP + k - j; /* window position of x_{i0 + k - j} */
+            const uint32_t pr = (lo & 1) ? W.O[(lo - 1) >> 1] : W.E[lo >> 1];
+            kk[j] = sdot2(pr, sg, kk[j]);
+        }
+    }
+}
+
 /* PATH_S16 candidate sums.  The dot chain of order p carries one extra tap, x[i] with
  * coefficient -2^sh, and starts from 2^31: t = 2^31 + pred - x[i]*2^sh.  That is exact in
  * [0, 2^32) (|x| <= 2^15, sh <= 15, |pred| < 2^26), so the logical shift t >> sh equals
@@ -1050,8 +1074,8 @@ __device__ __forceinline__ int rice_floor_log2(double x, const double* tl, const
  *  2. every thread, per chunk it owns: sum over the chunk of x >> p for each candidate
  *     order, parameters from pk of the chunk's finest partition (chunk_rice_bits);
  *  3. one wave reduction per order; thread 0 picks the order, first minimum (rice_finish). */
-template <bool INTLOG>
-__device__ __forceinline__ void rice_params_wave0(const ResidArgs& a, uint64_t s, const double* tl,
+template <bool INTLOG, typename ArgsT>
+__device__ __forceinline__ void rice_params_wave0(const ArgsT& a, uint64_t s, const double* tl,
                                                   unsigned long long* rb, int* misc, uint8_t* pk, int n, int order,
                                                   int rmin, int omax, int lane) {
     const int P = 1 << omax, k = lane;
@@ -1117,7 +1141,8 @@ __device__ __forceinline__ void chunk_rice_bits(const uint32_t (&z)[8], uint4 pv
 }
 
 /* reduce the per-thread data bits (each < 2^32), pick the order, write meta and parameters */
-__device__ __forceinline__ void rice_finish(const ResidArgs& a, flacmi_unit_meta* meta, const Decision* dec,
+template <typename ArgsT> /* ResidArgs, or the kernarg-segment view the looping variants read */
+__device__ __forceinline__ void rice_finish(const ArgsT& a, flacmi_unit_meta* meta, const Decision* dec,
                                             const uint32_t (&tb)[16], unsigned long long* rb,
                                             unsigned long long* red, int* misc, const uint8_t* pk, int n,
                                             int start, int rmin, int omax, int tid, int NT, int lane, int wid,
@@ -1198,6 +1223,12 @@ __device__ __forceinline__ KernargArgs opaque_args() {
     return p;
 }
 
+__device__ __forceinline__ uint32_t loop_tid() {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 template <int LMAX, int PATH, typename ResT, int VAR>
 __global__ __launch_bounds__(resid_launch_bound(PATH, LMAX, VAR)) void k_resid(ResidArgs a_in) {
     constexpr bool FAST = VAR == kVarFast;
@@ -1217,7 +1248,7 @@ __global__ __launch_bounds__(resid_launch_bound(PATH, LMAX, VAR)) void k_resid(R
     int32_t pre_st = 0, pre_rv0 = 0, pre_rv1 = 0; /* ... and its record's status and words tid, tid + NT */
 next_unit:
     auto&& a = [&]() -> decltype(auto) {
-        if constexpr (VAR == kVarMf8 || VAR == kVarList1) return *opaque_args();
+        if constexpr (VAR == kVarMf8 || VAR == kVarList || VAR == kVarList1) return *opaque_args();
         else return (a_in);
     }();
     if constexpr (VAR == kVarList || VAR == kVarList1) gid = a.retry_list[li];
@@ -1238,7 +1269,11 @@ next_unit:
     static_assert(!FAST || (MF && sizeof(ResT) == 4), "FAST: S16 MFMA path with a 32-bit residual only");
 
     extern __shared__ __align__(16) unsigned char smem[];
-    const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, nw = NT >> 6;
+    /* the looping variants re-read the thread id per unit (an asm the compiler cannot hoist):
+     * otherwise every value derived from it is hoisted out of the unit loop and held in
+     * registers across the whole body */
+    const int tid = (VAR == kVarList || VAR == kVarList1) ? (int)loop_tid() : (int)threadIdx.x;
+    const int NT = blockDim.x, lane = tid & 63, nw = NT >> 6;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6); /* wave-uniform: scalar loops */
     const int64_t u = a.unit0 + gid;
     const int n = a.n, L = a.L;
@@ -1691,8 +1726,92 @@ next_unit:
     A acc[NSUM];
 #pragma unroll
     for (int s = 0; s < NSUM; ++s) acc[s] = 0;
+    bool full_pass = true;
+    if constexpr (S16) {
+        /* Pruning mode, 16-bit samples (e.g. the units k_resid_stream hands over outside its
+         * MFMA bound): the exact fixed sums and the sign-correlation bound first (as
+         * mf8_candidate_sums does for 24-bit), the LPC chains only for a unit it leaves open */
+        if (do_lpc && a.prune && a.sign_bound && a.mode == FLACMI_MODE_REFERENCE && n >= 2 * HP) {
+            int32_t kk[LMAX + 1];
+#pragma unroll
+            for (int j = 0; j <= LMAX; ++j) kk[j] = 0;
+            uint32_t nneg = 0;
 #pragma unroll 1
-    for (int c = rice_only ? nch : tid; c < nch; c += NT) {
+            for (int c = tid; c < nch; c += NT) {
+                const int i0 = 8 * c;
+                Win16<HP> W;
+                W.load(xs16, i0);
+                if (i0 >= HP && i0 + 8 <= n) {
+                    chunk_sums_s16<LMAX, HP, false>(W, i0, n, L, false, cpair, lsh, acc);
+                    sb16_chunk<LMAX, HP>(W, kk, nneg); /* R' = the whole chunks inside [HP, n) */
+                } else {
+                    chunk_sums_s16<LMAX, HP, true>(W, i0, n, L, false, cpair, lsh, acc);
+                }
+            }
+            kk[0] -= (int32_t)nneg; /* K_0 - N_- */
+            /* per wave: the five fixed sums, then K_0 - N_-, K_1 .. K_LMAX (|K| per lane < 2^26) */
+            constexpr int RS1 = NSUM + 1;
+            uint32_t any = 0;
+#pragma unroll
+            for (int o = 0; o < 5; ++o) any |= acc[o];
+            const bool narrow = __ballot(any >= (1u << 26)) == 0;
+#pragma unroll
+            for (int o = 0; o < 5; ++o) {
+                const uint64_t v = narrow ? (uint64_t)wave_sum_u32((uint32_t)acc[o]) : wave_sum_u64((uint64_t)acc[o]);
+                if (lane == 0) red[wid * RS1 + o] = v;
+            }
+#pragma unroll
+            for (int j = 0; j <= LMAX; ++j) {
+                const uint32_t v = wave_sum_u32((uint32_t)kk[j]);
+                if (lane == 0) red[wid * RS1 + 5 + j] = (unsigned long long)(int64_t)(int32_t)v;
+            }
+            __syncthreads();
+            if (wid == 0) {
+                uint64_t tf = 0;
+                int64_t kt = 0;
+                if (lane < 5)
+                    for (int w2 = 0; w2 < nw; ++w2) tf += red[w2 * RS1 + lane];
+                if (lane <= LMAX)
+                    for (int w2 = 0; w2 < nw; ++w2) kt += (int64_t)red[w2 * RS1 + 5 + lane];
+                auto l64 = [&](uint64_t v, int l) __attribute__((always_inline)) -> uint64_t {
+                    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+                };
+                const uint64_t f0 = l64(tf, 0);
+                uint64_t fmin = f0;
+#pragma unroll
+                for (int o = 1; o < 5; ++o) fmin = l64(tf, o) < fmin ? l64(tf, o) : fmin;
+                const int64_t k0n = (int64_t)l64((uint64_t)kt, 0);
+                const int p = lane + 1;
+                int64_t S = 0;
+#pragma unroll
+                for (int j = 1; j <= LMAX; ++j) {
+                    const int64_t kj = (int64_t)l64((uint64_t)kt, j);
+                    const int32_t c = (p <= L && j <= p) ? cfl[lane * CT::CPAD + j - 1] : 0;
+                    S += (int64_t)c * kj;
+                }
+                bool lose = true; /* order p provably loses to the best fixed sum */
+                if (p <= L) {
+                    if (lsh[LMAX + lane] == 0) lose = f0 > fmin; /* coefficient-less: r = x, the order-0 sum */
+                    else lose = k0n - (S >> lsh[lane]) - 1 > (int64_t)fmin;
+                }
+                const bool decided = __ballot(!lose) == 0; /* every lane votes (outside the lane-0 store) */
+                if (lane == 0) misc[6] = decided ? 1 : 0;
+            }
+            __syncthreads();
+            if (misc[6]) {
+                full_pass = false;
+                lpc_pruned = true;
+                lpc_tiers = 1 << 8; /* "0/1": decided before the LPC pass */
+            } else {
+                lpc_tiers = 1 | (1 << 8);
+#pragma unroll
+                for (int s2 = 0; s2 < NSUM; ++s2) acc[s2] = 0;
+            }
+        }
+    }
+#pragma unroll 1
+    for (int c = rice_only || !full_pass ? nch : tid; c < nch; c += NT) {
         const int i0 = 8 * c;
         const bool fast = (i0 >= HP) && (i0 + 8 <= n);
         if constexpr (S16) {

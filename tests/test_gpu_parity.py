@@ -561,16 +561,21 @@ def test_lpc_pruning_paths_vs_oracle(az, q):
         _meta_params_residual_equal(prod, full, u)
     ok = om["status"] == 0
     pruned = pm["lpc_order"] == abi.LPC_PRUNED
-    if q == 5:  # (at q >= 9 these units exceed k_resid_stream's MFMA bound: k_resid never prunes)
+    if q == 5:  # (q >= 9 at L 12 takes the 64-bit path: no pruning there)
         assert pruned[:24].sum() >= 12, "config-2 units should mostly prune"
     # meta.lpc_tiers: k_resid_stream's quarter bound passes 1..4 (pruned) or 5 (the exact
-    # pass); 0 for units its retry list redid on k_resid (no pruning there)
+    # pass), x/4; for the units its retry list redid on k_resid, the 16-bit sign-correlation
+    # bound: 0/1 (pruned before the LPC pass) or 1/1 (the exact pass)
     tiers = pm["lpc_tiers"].astype(np.int64)
     st = tiers != 0
-    assert (tiers[st] >> 8 == 4).all()
-    assert (pruned[st] == ((tiers[st] & 0xff) <= 4)).all()
-    assert ((tiers[st] & 0xff) <= 5).all() and ((tiers[st] & 0xff) >= 1).all()
+    s4, s1 = st & (tiers >> 8 == 4), st & (tiers >> 8 == 1)
+    assert (s4 | s1 | ~st).all(), np.unique(tiers)
+    assert (pruned[s4] == ((tiers[s4] & 0xff) <= 4)).all()
+    assert ((tiers[s4] & 0xff) <= 5).all() and ((tiers[s4] & 0xff) >= 1).all()
+    assert (pruned[s1] == ((tiers[s1] & 0xff) == 0)).all() and ((tiers[s1] & 0xff) <= 1).all()
     assert not pruned[~st].any()
+    if q == 5:  # the LPC-winning units the stream kernel lists take the 16-bit bound's exact pass
+        assert (tiers == (1 | 1 << 8)).any(), np.unique(tiers)
     if q == 5:  # pruned after the first quarter, and after later ones
         assert (tiers == (1 | 4 << 8)).any() and ((tiers[st] & 0xff) >= 2).any(), np.unique(tiers)
     assert (ok & ~pruned & (om["kind"] == abi.KIND_FIXED)).any(), "no unit took the exact pass and chose fixed"
@@ -595,6 +600,16 @@ def test_production_batches_vs_oracle(az, cfg):
     pruned = out["meta"]["lpc_order"] == abi.LPC_PRUNED
     assert pruned.mean() > 0.9, pruned.mean()
     assert (ora["meta"]["kind"][pruned] == abi.KIND_FIXED).all()
+    if cfg == "c2":
+        # the units k_resid_stream lists (outside its MFMA bound) take k_resid's 16-bit
+        # sign-correlation bound over R' = [16, n): 0/1 exactly when the bound restated on the
+        # oracle's record decides, 1/1 (the exact LPC pass) otherwise
+        t = out["meta"]["lpc_tiers"].astype(np.int64)
+        listed = np.nonzero(t >> 8 == 1)[0]
+        assert len(listed) > 0 and (t[listed] == 1 << 8).any(), np.unique(t)
+        for u in listed:
+            want = sign_bound.decides(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u], lmax=16)
+            assert int(t[u]) == ((1 << 8) if want else (1 | 1 << 8)), (u, int(t[u]), want)
 
 
 # ---------------------------------------------------------------------------------------
