@@ -29,8 +29,10 @@ def _units(n, bits, seed):
     return np.ascontiguousarray(np.concatenate(rows))
 
 
-@pytest.mark.parametrize("n,bits,L,q", [(4096, 24, 32, 15), (16384, 24, 32, 12), (4608, 16, 32, 15)])
-def test_sign_bound_is_a_lower_bound(n, bits, L, q):
+@pytest.mark.parametrize("n,bits,L,q,lmax", [(4096, 24, 32, 15, 32), (16384, 24, 32, 12, 32), (4608, 16, 32, 15, 32),
+                                             (4608, 16, 12, 5, 16), (4608, 16, 12, 9, 16)])
+def test_sign_bound_is_a_lower_bound(n, bits, L, q, lmax):
+    """lmax 16: k_resid's 16-bit paths at L <= 12 take R' = [16, n) (k_resid.h sb16_chunk)."""
     a = _units(n, bits, n + q)
     ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, 8 if n % 256 == 0 else 5), n,
                                sample_bits=bits, threads=8)
@@ -40,10 +42,10 @@ def test_sign_bound_is_a_lower_bound(n, bits, L, q):
             continue
         rec, fs, ls = ora["lpc_records"][u], ora["fixed_sums"][u], ora["lpc_sums"][u]
         for hi in (None, n // 2, 4096):  # the whole R, and k_resid_sb's first tests ([lmax, hi))
-            for p, lb in enumerate(sign_bound.order_bounds(a[u], rec, L, hi=hi), start=1):
+            for p, lb in enumerate(sign_bound.order_bounds(a[u], rec, L, lmax=lmax, hi=hi), start=1):
                 if lb is not None:
                     assert lb <= int(ls[p - 1]), (u, p, hi, lb, int(ls[p - 1]))
-        if sign_bound.decides(a[u], rec, L, fs, split_end=n // 2):
+        if sign_bound.decides(a[u], rec, L, fs, lmax=lmax, split_end=n // 2):
             decided += 1
             assert int(ora["meta"]["lpc_sum"][u]) > int(ora["meta"]["fixed_sum"][u]), u
     assert decided > 0
