@@ -96,32 +96,43 @@ __global__ __launch_bounds__(256) void k_synth(T* dst, int32_t bits, int64_t str
 __global__ __launch_bounds__(256) void k_stats(const flacmi_unit_meta* __restrict__ meta, int64_t n_units,
                                                int32_t block_len, int32_t tail_len, int64_t n_tail_units,
                                                unsigned long long* stats) {
+    /* the scalar totals accumulate in registers over the grid-stride loop and are reduced once
+     * per wave; only the histograms use LDS atomics; one global atomic per nonzero word per
+     * workgroup (the grid is a few workgroups per CU: 2048 workgroups adding into the same 128
+     * words serialised at L2) */
     __shared__ unsigned long long h[FLACMI_STATS_WORDS];
     for (int i = threadIdx.x; i < FLACMI_STATS_WORDS; i += blockDim.x) h[i] = 0;
     __syncthreads();
+    unsigned long long cnt = 0, samples = 0, rice = 0, nfix = 0, nlpc = 0, npruned = 0, hash = 0;
     for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n_units; u += (int64_t)gridDim.x * blockDim.x) {
         const flacmi_unit_meta& m = meta[u];
         const int n = u >= n_units - n_tail_units ? tail_len : block_len;
-        atomicAdd(&h[0], 1ull);
-        atomicAdd(&h[1], (unsigned long long)n);
+        ++cnt;
+        samples += (unsigned long long)n;
         const int st = m.status & 15;
         atomicAdd(&h[64 + (m.status >= 16 ? 15 : st)], 1ull);
         if (m.status != 0) continue;
-        atomicAdd(&h[2], (unsigned long long)m.rice_bits);
+        rice += (unsigned long long)m.rice_bits;
         if (m.kind == FLACMI_KIND_FIXED) {
-            atomicAdd(&h[3], 1ull);
+            ++nfix;
             atomicAdd(&h[5 + (m.order & 7) % 5], 1ull);
         } else {
-            atomicAdd(&h[4], 1ull);
+            ++nlpc;
             atomicAdd(&h[9 + (m.order >= 1 && m.order <= 32 ? m.order : 32)], 1ull);
         }
         atomicAdd(&h[48 + (m.part_order & 15)], 1ull);
-        if (m.lpc_order == FLACMI_LPC_PRUNED) atomicAdd(&h[81], 1ull);
+        if (m.lpc_order == FLACMI_LPC_PRUNED) ++npruned;
         /* reference-visible results only (lpc_sum may be FLACMI_LPC_PRUNED) */
-        unsigned long long hsh = (unsigned long long)m.rice_bits * 0x9E3779B97F4A7C15ull ^
-                                 ((unsigned long long)m.fixed_sum << 1) ^
-                                 (unsigned long long)(m.kind * 64 + m.order) * 0xD1B54A32D192ED03ull;
-        atomicAdd(&h[80], hsh);
+        hash += (unsigned long long)m.rice_bits * 0x9E3779B97F4A7C15ull ^ ((unsigned long long)m.fixed_sum << 1) ^
+                (unsigned long long)(m.kind * 64 + m.order) * 0xD1B54A32D192ED03ull;
+    }
+    const unsigned long long v[7] = {cnt, samples, rice, nfix, nlpc, npruned, hash};
+    const int slot[7] = {0, 1, 2, 3, 4, 81, 80};
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        unsigned long long x = v[k];
+        for (int o = 32; o >= 1; o >>= 1) x += (unsigned long long)__shfl_xor(x, o);
+        if ((threadIdx.x & 63) == 0 && x) atomicAdd(&h[slot[k]], x);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < FLACMI_STATS_WORDS; i += blockDim.x)
@@ -231,7 +242,7 @@ hipError_t launch_stats(const flacmi_unit_meta* meta, int64_t n_units, int32_t b
                         int64_t n_tail_units, int64_t* stats, hipStream_t s) {
     if (n_units <= 0) return hipSuccess;
     int64_t blocks = (n_units + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > 512) blocks = 512; /* two workgroups per CU: fewer global atomics per word */
     hipLaunchKernelGGL(k_stats, dim3((unsigned)blocks), dim3(256), 0, s, meta, n_units, block_len, tail_len,
                        n_tail_units, (unsigned long long*)stats);
     return hipGetLastError();

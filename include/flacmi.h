@@ -180,7 +180,9 @@ typedef struct flacmi_unit_meta {
     int32_t lpc_tiers;       /* diagnostic, the pruning decision: LPC candidate passes made | passes of the
                                 path << 8.  16-bit stream kernel: quarter-block bound passes 1..4, then 5 =
                                 the exact pass; int8-MFMA path: eighths 2..8 of exact partial sums (8 = every
-                                tile).  0 where no pruning runs (fixed-only, all-candidates, other paths) */
+                                tile), 0/8 when the sign-correlation bound decides (k_resid_sb included);
+                                16-bit k_resid: 0/1 (sign bound decides) or 1/1 (the exact LPC pass).  0 where
+                                no pruning runs (fixed-only, all-candidates, the 64-bit chains) */
     int64_t fixed_sum;       /* sum(|r|) of the best fixed residual */
     int64_t lpc_sum;         /* sum(|r|) of the best LPC residual (0 in fixed-only mode, FLACMI_LPC_PRUNED if pruned) */
     int64_t rice_bits;       /* size estimate of the chosen partitioning (encoder.py:714-727) */
