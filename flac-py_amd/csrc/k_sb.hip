@@ -23,9 +23,10 @@ namespace flacmi {
  *      the rest of R, tested again; still undecided (or |x| > 2^23): the unit is listed for
  *      kVarList1, which redoes it with the planes and the tiers;
  *   4. decided: the first fixed argmin (LPC proven to lose, encoder.py:135-157), its
- *      residual as int32 difference chains to HBM with the finest partition sums, the Rice
- *      search (encoder.py:655-760) with the residual recomputed from the staged samples
- *      (no LDS copy of it), the meta record and the parameters.
+ *      residual as int32 difference chains to HBM and kept in registers (4 chunks x 8 per
+ *      thread), the finest partition sums by DPP steps, the Rice search (encoder.py:655-760)
+ *      over those registers (no LDS copy of the residual), the meta record and the
+ *      parameters.
  * ======================================================================================= */
 constexpr int kSbThreads = 512;
 constexpr int kSbChunks = 4; /* 8-sample chunks per thread at n <= 16384 */
