@@ -39,12 +39,16 @@ struct SbLds {
 constexpr int kSbRed = 16;
 /* K_j row sums: [32 rows (8 waves x 4 DPP rows)][stride] int32, lag j at column j */
 __host__ __device__ constexpr int sb_ks_stride(int lmax) { return ((lmax + 1 + 3) / 4) * 4; }
+/* LPC coefficients: one padded row per order (c_{p,1..p} at row p - 1, zeros after), rows
+ * 16-byte aligned and 36 words apart so wave 0's lanes read four coefficients per ds_read_b128
+ * across distinct banks */
+__host__ __device__ constexpr int sb_cf_stride(int lmax) { return lmax + 4; }
 __host__ __device__ inline SbLds sb_lds_layout(int lmax, int n, int P) {
     auto up = [](int b) { return (b + 15) & ~15; };
     SbLds l;
     int o = 0;
     l.xs = o;   o = up(o + 4 * (resid_hp(lmax) + n));
-    l.cf = o;   o = up(o + 4 * ((lmax * (lmax + 1)) / 2));
+    l.cf = o;   o = up(o + 4 * lmax * sb_cf_stride(lmax));
     l.red = o;  o = up(o + 8 * (kSbThreads / 64) * kSbRed);
     /* the K_j row sums are dead before the residual pass: they share the Rice region */
     l.ks = o;
@@ -95,10 +99,14 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
     /* ---- 1. staging: samples, record status / coefficient words / shifts, max|x| ---- */
     const int st = rec[0];
     const uint32_t negmask = (uint32_t)rec[1];
-    const int ntri = (L * (L + 1)) / 2;
-    int32_t cw[2];
+    constexpr int CFS = sb_cf_stride(LMAX), NCF = LMAX * CFS, KCF = (NCF + NT - 1) / NT;
+    int32_t cw[KCF]; /* padded-table entry tid + j NT: order row / CFS + 1, coefficient row % CFS */
 #pragma unroll
-    for (int j = 0; j < 2; ++j) cw[j] = rec[2 + L + min(tid + j * NT, ntri - 1)];
+    for (int j = 0; j < KCF; ++j) {
+        const int t = tid + j * NT, row = t / CFS, col = t - row * CFS, pp = row + 1;
+        const int32_t v = rec[min(2 + L + (pp * (pp - 1)) / 2 + col, a.rec_words - 1)];
+        cw[j] = (pp <= L && col < pp) ? v : 0;
+    }
     const int32_t shl = rec[2 + min(lane, L - 1)]; /* order lane + 1's shift (wave 0's test) */
     uint32_t xm = 0;
     {
@@ -124,8 +132,8 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
     }
     for (int i = tid; i < HP; i += NT) xs[i - HP] = 0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-        if (tid + j * NT < ntri) cf[tid + j * NT] = cw[j];
+    for (int j = 0; j < KCF; ++j)
+        if (tid + j * NT < NCF) cf[tid + j * NT] = cw[j];
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
         const uint32_t t = (uint32_t)__shfl_xor((int)xm, o);
@@ -273,13 +281,15 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
             for (int w2 = 0; w2 < nw; ++w2) kt += (int64_t)red[w2 * NR + 5];
         }
         const int64_t nneg = lane64(kt, LMAX + 1), k0 = lane64(kt, 0) + nneg;
-        const int pl = lane + 1, tb = (pl * (pl - 1)) / 2;
+        const int pl = lane + 1;
         int64_t S = 0;
-#pragma unroll 1
-        for (int j = 1; j <= L; ++j) {
-            const int64_t kj = lane64(kt, j) + nneg;
-            const int32_t c = (pl <= L && j <= pl) ? cf[tb + j - 1] : 0;
-            S += (int64_t)c * kj;
+        /* row pl - 1 holds c_{pl,1..pl} and zeros up to LMAX; lanes past LMAX read row 0 (unused) */
+        const int4v* crow = reinterpret_cast<const int4v*>(cf + (lane < LMAX ? lane : 0) * CFS);
+#pragma unroll 2
+        for (int jb = 0; jb < LMAX / 4; ++jb) {
+            const int4v c4 = crow[jb];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S += (int64_t)c4[e] * (lane64(kt, 4 * jb + e + 1) + nneg);
         }
         bool lose = true; /* this lane's order provably loses */
         if (pl <= L) {
