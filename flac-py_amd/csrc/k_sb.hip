@@ -63,7 +63,8 @@ __host__ __device__ inline SbLds sb_lds_layout(int lmax, int n, int P) {
     l.total = o;
     return l;
 }
-template <int LMAX>
+/* R08: Rice orders 0..8 (config 3: rmin 0, finest order 8), compile-time order loops */
+template <int LMAX, bool R08>
 __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_resid_sb(ResidArgs a) {
     constexpr int HP = resid_hp(LMAX), NT = kSbThreads, nw = NT / 64, NR = kSbRed, KS = sb_ks_stride(LMAX);
     static_assert(HP >= LMAX && LMAX % 4 == 0, "the bound's window reads LMAX samples of history");
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t gid = blockIdx.x;
     const int n = a.n, L = a.L, nch = n >> 3;
-    const int omax = sb_finest_order(n, a.rmin, a.rmax);
+    const int omax = R08 ? 8 : sb_finest_order(n, a.rmin, a.rmax);
     const int P = 1 << omax, cpp = (n >> omax) >> 3;
     const SbLds lay = sb_lds_layout(LMAX, n, P);
     int32_t* xs = reinterpret_cast<int32_t*>(smem + lay.xs) + HP; /* [-HP, n) */
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
         }
         __syncthreads();
         if (a.stop_after == 4) return;
-        const int ro = __builtin_amdgcn_readfirstlane(a.rmin), oo = __builtin_amdgcn_readfirstlane(omax);
+        const int ro = R08 ? 0 : __builtin_amdgcn_readfirstlane(a.rmin), oo = R08 ? 8 : __builtin_amdgcn_readfirstlane(omax);
         /* prefix sums of the finest sums (wave 0), then every heap node's parameter, one node
          * per thread, header bits per order, the first error in the reference's evaluation
          * order by atomicMin (see k_resid's wide Rice step) */
@@ -580,7 +581,8 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
 hipError_t launch_resid_sb_kernel(const ResidArgs& a, int lmax, hipStream_t s) {
     const int om = sb_finest_order(a.n, a.rmin, a.rmax);
     const size_t lds = sb_lds_layout(lmax, a.n, 1 << om).total;
-    auto ks = lmax == 16 ? k_resid_sb<16> : k_resid_sb<32>;
+    const bool r08 = a.rmin == 0 && om == 8;
+    auto ks = lmax == 16 ? (r08 ? k_resid_sb<16, true> : k_resid_sb<16, false>) : (r08 ? k_resid_sb<32, true> : k_resid_sb<32, false>);
     hipError_t e = hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(ks, dim3((unsigned)a.count), dim3(kSbThreads), lds, s, a);
