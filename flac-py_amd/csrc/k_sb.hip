@@ -73,7 +73,7 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t gid = blockIdx.x;
-    const int n = NFIX ? NFIX : a.n, L = a.L, nch = n >> 3;
+    const int n = NFIX ? NFIX : a.n, L = NFIX ? LMAX : a.L, nch = n >> 3; /* NFIX variants: L = LMAX */
     const int omax = R08 ? 8 : sb_finest_order(n, a.rmin, a.rmax);
     const int P = 1 << omax, cpp = (n >> omax) >> 3;
     const SbLds lay = sb_lds_layout(LMAX, n, P);
@@ -584,7 +584,8 @@ hipError_t launch_resid_sb_kernel(const ResidArgs& a, int lmax, hipStream_t s) {
     const size_t lds = sb_lds_layout(lmax, a.n, 1 << om).total;
     const bool r08 = a.rmin == 0 && om == 8;
     auto ks = lmax == 16 ? (r08 ? k_resid_sb<16, true> : k_resid_sb<16, false>)
-                         : (r08 ? (a.n == 16384 ? k_resid_sb<32, true, 16384> : k_resid_sb<32, true>) : k_resid_sb<32, false>);
+                         : (r08 ? (a.n == 16384 && a.L == 32 ? k_resid_sb<32, true, 16384> : k_resid_sb<32, true>)
+                                : k_resid_sb<32, false>);
     hipError_t e = hipFuncSetAttribute((const void*)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(ks, dim3((unsigned)a.count), dim3(kSbThreads), lds, s, a);

@@ -51,7 +51,7 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 #endif
 constexpr int kSCPT = FLACMI_STREAM_CPT; /* max 8-sample chunks per thread */
 /* workgroup size: 8-sample chunks, up to kSCPT per thread */
-__host__ __device__ inline int stream_threads(int n) {
+__host__ __device__ constexpr int stream_threads(int n) {
     const int nch = n / 8;
     const int nt = 64 * ((nch + 64 * kSCPT - 1) / (64 * kSCPT));
     return nt < 64 ? 64 : nt;
@@ -311,10 +311,12 @@ __device__ __forceinline__ void store_meta(flacmi_unit_meta* m, int lane, const 
  * every predictor order), so the order loops compile without per-order branches.  One
  * workgroup per unit; every exit is workgroup-uniform (all waves decide from the same LDS
  * data). */
-template <int NG, bool R05>
+template <int NG, bool R05, int NFIX = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7, 8))) void k_resid_stream(ResidArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int tid = threadIdx.x, NT = blockDim.x, lane = tid & 63, nw = NT >> 6;
+    /* NFIX: the block length (and L = 4 NG, the workgroup size) as compile-time constants, the
+     * BASELINE configs' 4608-sample units: loop bounds, chunk guards and partition indices fold */
+    const int tid = threadIdx.x, NT = NFIX ? stream_threads(NFIX) : (int)blockDim.x, lane = tid & 63, nw = NT >> 6;
 #if FLACMI_STREAM_STAMPS /* diagnostic build only: per-unit phase clock stamps of wave 0 */
     uint64_t stamp[8];
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
@@ -325,9 +327,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
 #endif
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t gid = blockIdx.x;
-    const int n = a.n, L = NG > 0 ? a.L : 0;
+    const int n = NFIX ? NFIX : a.n, L = NG > 0 ? (NFIX ? 4 * NG : a.L) : 0;
     const int nch = n >> 3, nblk = n >> 6;
-    const int rw = NG > 0 ? a.rec_words : 0;
+    const int rw = NG > 0 ? (NFIX ? 2 + L + (L * (L + 1)) / 2 : a.rec_words) : 0;
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (n % (1 << o) == 0) rmax_eff = o;
@@ -367,7 +369,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
         constexpr int kTW = tap_table_words(NG), kTJ = NG > 0 ? (kTW + 63) / 64 : 0;
         int32_t tv[kTJ > 0 ? kTJ : 1][2];
         if constexpr (NG > 0) {
-            const int32_t* r = a.rec + gid * a.rec_words;
+            const int32_t* r = a.rec + gid * rw;
 #pragma unroll
             for (int j = 0; j < kTJ; ++j) {
                 if (j > 0 && j * NT >= kTW) break; /* uniform: a two-wave unit needs j = 0 only */
@@ -420,7 +422,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     /* ---- unit status from the LPC record; MFMA exactness bound per order.
      * Every wave reads the same LDS words, so the exits are workgroup-uniform. ---- */
     uint32_t negmask = 0;
-    const int32_t* __restrict__ grec = NG > 0 ? a.rec + gid * a.rec_words : nullptr; /* wave-uniform: scalar loads */
+    const int32_t* __restrict__ grec = NG > 0 ? a.rec + gid * rw : nullptr; /* wave-uniform: scalar loads */
     if constexpr (NG > 0) {
         const int st = grec[0];
         if (st != 0) { /* the reference raises inside encode_subframe_lpc */
@@ -1050,8 +1052,25 @@ bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes) {
     return true;
 }
 
+template <int NG, int NFIX>
+static hipError_t launch_stream_F(const ResidArgs& a, hipStream_t s) {
+    constexpr int nt = stream_threads(NFIX);
+    int rmax_eff = -1;
+    for (int o = a.rmin; o <= a.rmax; ++o)
+        if (a.n % (1 << o) == 0) rmax_eff = o;
+    const size_t lds = stream_lds(a.n, nt / 64, tap_table_words(NG), 1 << rmax_eff, kRiceOrders).total;
+    auto kern = k_resid_stream<NG, true, NFIX>;
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)a.count), dim3(nt), lds, s, a);
+    return hipGetLastError();
+}
+
 template <int NG, bool R05>
 static hipError_t launch_stream_R(const ResidArgs& a, hipStream_t s) {
+    if constexpr (R05) /* the BASELINE configs' 4608-sample units at L = 4 NG: the constant-shape build */
+        if (a.n == 4608 && (NG == 0 || a.L == 4 * NG) && getenv("FLACMI_STREAM_GENERIC") == nullptr)
+            return launch_stream_F<NG, 4608>(a, s);
     const int nt = stream_threads(a.n);
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
