@@ -188,31 +188,40 @@ __global__ __launch_bounds__(kSbThreads) __attribute__((amdgpu_waves_per_eu(4)))
     constexpr int split = kSbSplit;
     {
         uint64_t fa[5] = {0, 0, 0, 0, 0};
-        int k = 0;
-#pragma unroll 1
-        for (int c = tid; c < nch; c += NT, ++k) {
-            const int i0 = 8 * c;
-            int32_t x12[12];
+        auto fixed_chunk_sums = [&](const int32_t (&x12)[12], int i0) __attribute__((always_inline)) {
             uint32_t ca[5] = {0, 0, 0, 0, 0};
-            if (k < split) {
-                int32_t xw[LMAX + 8];
-                load_window(i0, xw);
-#pragma unroll
-                for (int e = 0; e < 12; ++e) x12[e] = xw[LMAX - 4 + e];
-                if (i0 >= LMAX) bound_chunk(xw);
-            } else {
-                const int4v* w4 = reinterpret_cast<const int4v*>(xs + i0 - 4);
-#pragma unroll
-                for (int g = 0; g < 3; ++g) {
-                    const int4v v = w4[g];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) x12[4 * g + e] = v[e];
-                }
-            }
             if (i0 >= 8) fixed_sums32<false>(x12, i0, n, ca);
             else fixed_sums32<true>(x12, i0, n, ca);
 #pragma unroll
             for (int o = 0; o < 5; ++o) fa[o] += ca[o];
+        };
+        /* the first split chunks of each thread: the bound's terms beside the fixed sums */
+#pragma unroll 1
+        for (int k = 0; k < split; ++k) {
+            const int c = tid + k * NT;
+            if (c >= nch) break;
+            const int i0 = 8 * c;
+            int32_t xw[LMAX + 8];
+            load_window(i0, xw);
+            int32_t x12[12];
+#pragma unroll
+            for (int e = 0; e < 12; ++e) x12[e] = xw[LMAX - 4 + e];
+            if (i0 >= LMAX) bound_chunk(xw);
+            fixed_chunk_sums(x12, i0);
+        }
+        /* the rest: fixed sums only */
+#pragma unroll 1
+        for (int c = tid + split * NT; c < nch; c += NT) {
+            const int i0 = 8 * c;
+            const int4v* w4 = reinterpret_cast<const int4v*>(xs + i0 - 4);
+            int32_t x12[12];
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                const int4v v = w4[g];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x12[4 * g + e] = v[e];
+            }
+            fixed_chunk_sums(x12, i0);
         }
         uint64_t any = 0;
 #pragma unroll
