@@ -72,6 +72,29 @@ __global__ __launch_bounds__(256) void k_synth(T* dst, int32_t bits, int64_t str
         st[k] = 256u * dphi[k];
         a32[k] = (int32_t)amp[k];
     }
+    if (bits <= 24) {
+        /* every intermediate fits 32 bits here: |s| < 3 * 2^14, the noise term < 2^12, and
+         * (s + noise) * 2^(bits - 16) < 2^25; the byte sum is one v_sad_u8 */
+        const int32_t lo32 = (int32_t)lo, hi32 = (int32_t)hi, sg = (int32_t)sigma;
+        const int e = bits > 16 ? bits - 16 : 0;
+        const uint32_t emask = (1u << e) - 1u;
+        const int32_t ehalf = e > 0 ? (1 << (e - 1)) : 0;
+        for (int i = threadIdx.x; i < len; i += 256) {
+            int32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                acc += __mul24(a32[k], tab[ph[k] >> 20]);
+                ph[k] += st[k];
+            }
+            const uint64_t r = splitmix64(seed ^ ((uint64_t)unit << 32) ^ (uint64_t)i);
+            const int32_t bsum = (int32_t)__builtin_amdgcn_sad_u8((uint32_t)r, 0u, 0u);
+            int32_t v = (acc >> 15) + (__mul24(bsum - 510, sg) >> 7);
+            if (bits > 16) v = v * (1 << e) + (int32_t)((uint32_t)(r >> 32) & emask) - ehalf;
+            else if (bits < 16) v >>= (16 - bits);
+            dst[uu * stride + i] = (T)(v < lo32 ? lo32 : (v > hi32 ? hi32 : v));
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < len; i += 256) {
         int32_t acc = 0;
 #pragma unroll

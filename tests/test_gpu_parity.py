@@ -216,7 +216,9 @@ def test_device_lpc_sites_from_acf_rows(az):
 def test_synth_device_matches_oracle(az):
     import ctypes as C
     n_units, n = 9, 4608
-    for bits, dt in ((16, np.int16), (24, np.int32)):
+    # bits <= 24: the 32-bit path of k_synth; 28 and 31 (the widest it takes): its int64 path
+    for bits, dt in ((8, np.int16), (12, np.int16), (16, np.int16), (20, np.int32), (24, np.int32),
+                     (28, np.int32), (31, np.int32)):
         nbytes = np.dtype(dt).itemsize
         d = az.lib.flacmi_device_alloc(az.ctx, n_units * n * nbytes)
         az.synth_device(d, nbytes, bits, n, 5, n_units, n, 42)
