@@ -631,7 +631,7 @@ template <int MAXC> /* chunks per thread the launch guarantees (2..kMaxC): fewer
                      * frames in flight per CU */
 __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
     __shared__ uint32_t win[kWinWords];
-    __shared__ uint16_t ct[4 * 256];
+    __shared__ __align__(16) uint16_t ct[4 * 256];
     __shared__ uint8_t hdr[16];
     __shared__ uint32_t sub_start[9];
     __shared__ int32_t cnt14[8];
@@ -650,7 +650,8 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
     const int C = a.channels;
     const uint32_t A = (uint32_t)(8 * (F & 3)); /* aligned bit of the frame's first bit */
     const int nwf = (int)(((F & 3) + (Fend - F) + 3) >> 2); /* window words of the frame */
-    for (int i = tid; i < 4 * 256; i += NT) ct[i] = a.crc_slice[i];
+    /* the 2 KB of CRC slice tables as 128 16-byte loads (not 1024 2-byte ones) */
+    for (int i = tid; i < 128; i += NT) reinterpret_cast<uint4*>(ct)[i] = reinterpret_cast<const uint4*>(a.crc_slice)[i];
     for (int i = tid; i < nwf; i += NT) win[i] = 0;
     if (tid < 8) cnt14[tid] = 0;
     if (tid == 0) hb_s = frame_header(a.first_frame + f, unit_len(a, u0), hdr);
