@@ -107,6 +107,31 @@ def test_c2_shape_batch(az):
     batch_case(az, 192, 4608, 16, 2024, 12, 5, 0, 5)
 
 
+@pytest.mark.parametrize("L,mode", [(12, abi.MODE_REFERENCE), (8, abi.MODE_REFERENCE), (0, abi.MODE_FIXED_ONLY)])
+def test_stream_constant_and_runtime_shape_builds_agree(az, monkeypatch, L, mode):
+    """4608-sample units take k_resid_stream's constant-shape build; FLACMI_STREAM_GENERIC=1
+    takes the runtime-shape build.  Both against the oracle, in production (pruning) mode and
+    with every candidate exact, and field for field against each other."""
+    n = 4608
+    a = oracle.synth_batch(700, 96, n, 16, 31 + L, dtype=np.int16)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, 5, 0, 5, mode), n, sample_bits=16, threads=16)
+    runs = {}
+    for generic in (False, True):
+        if generic:
+            monkeypatch.setenv("FLACMI_STREAM_GENERIC", "1")
+        else:
+            monkeypatch.delenv("FLACMI_STREAM_GENERIC", raising=False)
+        for debug in (False, True):
+            out = az.analyze(a, make_params(L, 5, 0, 5, mode), n, sample_bits=16, debug=debug)
+            compare_with_oracle(out, ora, [n] * len(a))
+            runs[(generic, debug)] = out
+    monkeypatch.delenv("FLACMI_STREAM_GENERIC", raising=False)
+    for debug in (False, True):
+        x, y = runs[(False, debug)], runs[(True, debug)]
+        assert np.array_equal(x["meta"], y["meta"]) and np.array_equal(x["rice_params"], y["rice_params"])
+        assert np.array_equal(x["residual"], y["residual"])
+
+
 @pytest.mark.parametrize("q", [6, 7, 9, 15])
 def test_c2_shape_fast_kernel_and_retry_list(az, q):
     """config 2 shape at higher precisions: the fast S16 MFMA kernel takes the units inside
