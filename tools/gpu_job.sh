@@ -2,5 +2,5 @@
 # other tools/gpu_*.sh, pmc_*.sh and profile.sh)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r6h; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?; tail -1 $O/pytest_gpu.log; [ $rc -eq 0 ] || { grep -B5 -A30 "FAILED\|Error" $O/pytest_gpu.log | head -80; exit 1; }
+STOPS="1 2 4 5 6 7 0" KPAT=k_resid_sb bash tools/pmc_stops.sh r6i insts --config c3 --e2e-units 0 > /dev/null && STOPS="1 2 4 5 6 7 0" bash tools/ablate.sh r6i/abl --config c3
+for k in 1 2 4 5 6 7 0; do python3 tools/pmc_summary.py gpurun_out/r6i/s$k | grep -A9 k_resid_sb | grep "INSTS_VALU\|INSTS_SALU" | tr '\n' ' '; echo " stop $k"; done
