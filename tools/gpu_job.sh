@@ -2,5 +2,7 @@
 # other tools/gpu_*.sh, pmc_*.sh and profile.sh)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-STOPS="1 2 4 5 6 7 0" KPAT=k_resid_sb bash tools/pmc_stops.sh r6i insts --config c3 --e2e-units 0 > /dev/null && STOPS="1 2 4 5 6 7 0" bash tools/ablate.sh r6i/abl --config c3
-for k in 1 2 4 5 6 7 0; do python3 tools/pmc_summary.py gpurun_out/r6i/s$k | grep -A9 k_resid_sb | grep "INSTS_VALU\|INSTS_SALU" | tr '\n' ' '; echo " stop $k"; done
+O=gpurun_out/r5final2; mkdir -p $O
+timeout -k 10 400 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { tail -20 $O/bench_c2.err; exit 1; }
+python3 -c "import json; d=json.load(open('$O/bench_c2.json')); r=d['roofline']; print(d['value'], d['ms_per_step'], r['frac'], r['traffic_current'], r['library_sha16'], r.get('traffic_library_sha16'))"
+for c in c3 c5; do timeout -k 10 400 python bench.py --config $c --steps 3 --warmup 1 --cpu-seconds 3 > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }; python3 -c "import json; d=json.load(open('$O/bench_$c.json')); r=d['roofline']; print('$c', d['value'], r['frac'], r['traffic_current'])"; done
