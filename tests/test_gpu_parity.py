@@ -715,6 +715,27 @@ def _sb_lean(n, rmax=8):
     return 8192 <= n <= 16384 and n % 256 == 0 and 6 <= om <= 8 and (n >> om) % 8 == 0 and cpp & (cpp - 1) == 0
 
 
+@pytest.mark.parametrize("n,L,rmax", [(16384, 32, 8), (8192, 32, 8), (8192, 32, 7), (8192, 32, 6),
+                                     (16384, 16, 8), (16384, 20, 7)])
+def test_sb_builds_vs_oracle(az, n, L, rmax):
+    """k_resid_sb's builds through production calls against the oracle: the config-3 constant
+    build (16384 samples, L 32, Rice orders 0..8), the orders-0..8 build at runtime n and L,
+    and the generic build (finest order 6 or 7).  A unit the bound decides reports 0/8 tiers
+    and must lose to fixed in the oracle; every unit matches the oracle field for field."""
+    assert _sb_lean(n, rmax)
+    a = oracle.synth_batch(3000, 40, n, 24, 7 + n // 1024 + L + rmax, dtype=np.int32)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, 15, 0, rmax), n, sample_bits=24, threads=16)
+    out = az.analyze(a, make_params(L, 15, 0, rmax), n, sample_bits=24)
+    compare_with_oracle(out, ora, [n] * len(a))
+    pm = out["meta"]
+    pruned = pm["lpc_order"] == abi.LPC_PRUNED
+    assert pruned.mean() > 0.5, pruned.mean()
+    assert (pm["lpc_tiers"][pruned] == 8 << 8).all()
+    assert (ora["meta"]["kind"][pruned] == abi.KIND_FIXED).all()
+    for u in np.nonzero(pruned)[0]:
+        assert _emulate_sign_bound(a[u], ora["lpc_records"][u], L, ora["fixed_sums"][u], lean=True), u
+
+
 def _emulate_sign_bound(x, rec, L, fixed_sums, lmax=32, lean=False):
     """The sign-correlation bound of mf8_candidate_sums / k_resid_sb restated on the oracle's
     record (tests/sign_bound.py) -> True when every order loses to the best fixed sum."""
