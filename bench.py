@@ -615,7 +615,13 @@ def main(argv=None):
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # checker only
         rng = np.random.default_rng(args.seed)
-        pick = np.sort(rng.choice(units, size=min(args.parity_units, units), replace=False))
+        pick = rng.choice(units, size=min(args.parity_units, units), replace=False)
+        # plus up to 8 units of every pruning path the batch took (meta.lpc_tiers: quarter or
+        # eighth tiers, the sign bound's passes, the retry list's 0/1 and 1/1, exact passes)
+        tiers_all = meta_np["lpc_tiers"].astype(np.int64)
+        extra = [rng.choice(np.nonzero(tiers_all == t)[0], size=min(8, int((tiers_all == t).sum())), replace=False)
+                 for t in np.unique(tiers_all)]
+        pick = np.unique(np.concatenate([pick] + extra))
         s_host = samples[torch.as_tensor(pick, device=dev)].cpu().numpy()[:, :n]
         ora = oracle.analyze_batch(np.ascontiguousarray(s_host), oracle.make_params(cfg["L"], cfg["q"], cfg["rmin"],
                                    cfg["rmax"], cfg["mode"]), n, sample_bits=bits, threads=16)
@@ -631,7 +637,8 @@ def main(argv=None):
             k = int(o["n_parts"])
             same = same and np.array_equal(par_host[j][:k], ora["rice_params"][j][:k])
             bad += 0 if same else 1
-        parity = {"units_checked": int(len(pick)), "mismatches": bad, "lpc_pruned": pruned,
+        covered = {f"{t & 0xff}/{t >> 8}": int((tiers_all[pick] == t).sum()) for t in np.unique(tiers_all)}
+        parity = {"units_checked": int(len(pick)), "mismatches": bad, "lpc_pruned": pruned, "lpc_tiers_checked": covered,
                   "check": "meta, coefficients, zig-zag residual and Rice parameters bit-exact vs oracle "
                            "(a unit reporting FLACMI_LPC_PRUNED must lose to fixed in the oracle too)"}
 
