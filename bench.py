@@ -603,6 +603,29 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     kt = az.timing()
     elapsed = reduce_elapsed(elapsed, dist, dev)
+    kt_steps, isolated_calls = kt, 0
+    if cfg["L"] > 0 and not cfg["mode"] and os.environ.get("FLACMI_OVERLAP", "") != "0":
+        # The library's default chunking overlaps k_lpc's last, partly filled round with
+        # k_resid of the first chunk (flacmi_host.cpp overlap_mode), so the timed
+        # steps' stage spans include the other kernel's waves.  The roofline prices each kernel
+        # on launches of its own: a few more calls with one chunk (FLACMI_OVERLAP=0, read per
+        # call), after the timed region.
+        prev = os.environ.get("FLACMI_OVERLAP")
+        os.environ["FLACMI_OVERLAP"] = "0"
+        try:
+            step()
+            torch.cuda.synchronize(dev)
+            az.timing_reset()
+            isolated_calls = max(1, min(args.steps, 5))
+            for _ in range(isolated_calls):
+                step()
+            torch.cuda.synchronize(dev)
+            kt = az.timing()
+        finally:
+            if prev is None:
+                del os.environ["FLACMI_OVERLAP"]
+            else:
+                os.environ["FLACMI_OVERLAP"] = prev
 
     meta_np = meta.cpu().numpy().view(abi.META_DTYPE).reshape(units)
     st = stats.cpu().numpy()
@@ -713,12 +736,18 @@ def main(argv=None):
                                             "frac": ab_ws[dominant] / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                                             if dom_ms else None},
                          # the whole analysis step (k_lpc + k_resid + retries): SURVEY 8d bytes / call time
-                         "pipeline_frac": (pipe_b / (kt["call_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS) if kt["call_ms"] else None,
+                         "pipeline_frac": (pipe_b / (kt_steps["call_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                         if kt_steps["call_ms"] else None,
                          "pipeline_algorithmic_bytes": pipe_b},
             "kernels": {"k_lpc_ms": kt["lpc_ms"], "k_resid_ms": kt["resid_ms"], "call_ms": kt["call_ms"],
                         "k_lpc_GBs": lpc_gbs, "k_resid_GBs": resid_gbs,
-                        "pipeline_GBs": pipe_b / (kt["call_ms"] * 1e-3) / 1e9 if kt["call_ms"] else 0.0,
-                        "timed_calls": kt["calls"]},
+                        "pipeline_GBs": pipe_b / (kt_steps["call_ms"] * 1e-3) / 1e9 if kt_steps["call_ms"] else 0.0,
+                        "timed_calls": kt["calls"],
+                        "launches": ("one chunk per call (FLACMI_OVERLAP=0): %d calls after the timed steps, "
+                                     "whose calls overlap k_lpc's last round with k_resid" % isolated_calls)
+                        if isolated_calls else "the timed steps' calls",
+                        "timed_steps": {"call_ms": kt_steps["call_ms"], "k_lpc_span_ms": kt_steps["lpc_ms"],
+                                        "k_resid_span_ms": kt_steps["resid_ms"]} if isolated_calls else None},
             "cpu_baseline": cpu,
             "frame_writer": frames,
             "end_to_end": e2e,

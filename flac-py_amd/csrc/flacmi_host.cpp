@@ -438,15 +438,16 @@ static int prune_allowed() {
     return v;
 }
 
-/* FLACMI_OVERLAP=k (k > 1): k_lpc and k_resid of consecutive chunks overlap on two
- * streams (see analyze_device_impl); chunks hold at least kOverlapMinUnits units. */
+/* k_lpc and k_resid of consecutive chunks overlap on two streams (see analyze_device_impl).
+ * FLACMI_OVERLAP (read per call): unset or -1 = round-aligned (the default): the units of
+ * k_lpc's whole rounds, then the remainder (a partly filled last round), whose k_lpc runs
+ * beside k_resid of the first chunk, when the remainder holds at least kOverlapMinUnits;
+ * 0 = no overlap; k > 1 = up to k equal chunks of at least kOverlapMinUnits; -R (R > 1) =
+ * round-aligned with R units per round and no minimum (tests). */
 constexpr int64_t kOverlapMinUnits = 16384;
-static int overlap_chunks() {
-    static const int v = [] {
-        const char* e = getenv("FLACMI_OVERLAP");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
+static int overlap_mode() {
+    const char* e = getenv("FLACMI_OVERLAP");
+    return e && e[0] ? atoi(e) : -1;
 }
 
 static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi_params* p,
@@ -485,11 +486,33 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         int64_t unit0, count;
         int n;
     } ch[flacmi_ctx::kMaxChunks];
+    auto lpc_params_for = [&](int n) {
+        LpcArgs a{};
+        a.stride = b->unit_stride;
+        a.sample_bytes = b->sample_bytes;
+        a.n = n;
+        a.L = L;
+        return a;
+    };
     int nch = 0;
-    const int want = lpc && overlap_chunks() > 1 ? overlap_chunks() : 1;
-    const bool overlap = want > 1 && b->n_units >= 2 * kOverlapMinUnits;
+    const int ov = lpc ? overlap_mode() : 0;
+    const int want = ov > 1 ? ov : 1;
+    bool overlap = want > 1 && b->n_units >= 2 * kOverlapMinUnits;
     for (int c = 0; c < ncls; ++c) {
-        int64_t k = overlap ? cls[c].count / kOverlapMinUnits : 1;
+        if (ov < 0) {
+            /* round-aligned: the units of k_lpc's whole rounds, then the remainder, whose
+             * k_lpc fills the last round's idle slots beside k_resid of the first chunk */
+            const int64_t R = ov < -1 ? -(int64_t)ov : lpc_units_per_round(lpc_params_for(cls[c].n));
+            const int64_t whole = R > 0 ? cls[c].count / R * R : 0, rest = cls[c].count - whole;
+            if (whole > 0 && rest > 0 && (ov < -1 || rest >= kOverlapMinUnits) &&
+                nch + 2 + (ncls - 1 - c) <= flacmi_ctx::kMaxChunks) {
+                ch[nch++] = {cls[c].unit0, whole, cls[c].n};
+                ch[nch++] = {cls[c].unit0 + whole, rest, cls[c].n};
+                overlap = true;
+                continue;
+            }
+        }
+        int64_t k = overlap && ov > 1 ? cls[c].count / kOverlapMinUnits : 1;
         const int left = flacmi_ctx::kMaxChunks - nch - (ncls - 1 - c);
         k = k < 1 ? 1 : k > want ? want : k;
         k = k > left ? left : k;

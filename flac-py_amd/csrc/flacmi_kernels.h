@@ -128,6 +128,9 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes);
 constexpr int kMaxFinestParts = 4096;
 
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);
+/* units one full round of launch_lpc's kernel covers on the current device (resident
+ * workgroups per CU x 256 units x CUs); 0 when the occupancy query fails */
+int64_t lpc_units_per_round(const LpcArgs& a);
 /* test knob: fill every CU's LDS with a pattern (env FLACMI_POISON_LDS), else nothing */
 hipError_t launch_poison_lds(hipStream_t s);
 /* copy nf + 1 frame offsets and nf statuses to mapped host memory (k_misc.hip) */

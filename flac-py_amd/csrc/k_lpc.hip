@@ -527,6 +527,25 @@ hipError_t launch_lpc_from_acf(const LpcArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int LMAX>
+static const void* lpc_kernel_T(const LpcArgs& a) {
+    if constexpr (LMAX <= 12)
+        if (a.sample_bytes == 2 && lpc_tile_enabled() && a.stride % 8 == 0 && a.stride >= 8)
+            return reinterpret_cast<const void*>(&k_lpc_tile<LMAX>);
+    return a.sample_bytes == 2 ? reinterpret_cast<const void*>(&k_lpc<LMAX, int16_t>)
+                               : reinterpret_cast<const void*>(&k_lpc<LMAX, int32_t>);
+}
+
+int64_t lpc_units_per_round(const LpcArgs& a) {
+    const void* f = a.L <= 4 ? lpc_kernel_T<4>(a) : a.L <= 8 ? lpc_kernel_T<8>(a) : a.L <= 12 ? lpc_kernel_T<12>(a)
+                  : a.L <= 16 ? lpc_kernel_T<16>(a) : lpc_kernel_T<32>(a);
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 256, 0) != hipSuccess)
+        return 0;
+    return (int64_t)nb * 256 * cus;
+}
+
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s) {
     if (a.count <= 0) return hipSuccess;
     if (a.L <= 4) return launch_lpc_T<4>(a, s);

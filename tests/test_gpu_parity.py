@@ -132,6 +132,38 @@ def test_stream_constant_and_runtime_shape_builds_agree(az, monkeypatch, L, mode
         assert np.array_equal(x["residual"], y["residual"])
 
 
+@pytest.mark.parametrize("shape", ["c2q6", "c3"])
+def test_round_aligned_overlap_chunks(az, monkeypatch, shape):
+    """The default chunking (flacmi_host.cpp overlap_mode): k_lpc's whole rounds, then the
+    remainder, whose k_lpc runs on the side stream beside k_resid of the first chunk.
+    FLACMI_OVERLAP=-R forces R units per round, so a small batch splits: against the oracle
+    and field for field against FLACMI_OVERLAP=0 (one chunk), production and debug calls.
+    q 6 at config 2 sends about a third of the units of both chunks through the stream kernel's
+    retry list."""
+    if shape == "c3":
+        n, bits, L, q, rmax, units, R, dt = 16384, 24, 32, 15, 8, 40, 24, np.int32
+    else:
+        n, bits, L, q, rmax, units, R, dt = 4608, 16, 12, 6, 5, 200, 128, np.int16
+    a = oracle.synth_batch(1300, units, n, bits, 77, dtype=dt)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, rmax), n, sample_bits=bits, threads=16)
+    runs = {}
+    for ov in ("0", "-%d" % R):
+        monkeypatch.setenv("FLACMI_OVERLAP", ov)
+        for debug in (False, True):
+            out = az.analyze(a, make_params(L, q, 0, rmax), n, sample_bits=bits, debug=debug)
+            compare_with_oracle(out, ora, [n] * units)
+            runs[(ov, debug)] = out
+    monkeypatch.delenv("FLACMI_OVERLAP", raising=False)
+    for debug in (False, True):
+        x, y = runs[("0", debug)], runs[("-%d" % R, debug)]
+        assert np.array_equal(x["meta"], y["meta"]) and np.array_equal(x["rice_params"], y["rice_params"])
+        assert np.array_equal(x["residual"], y["residual"])
+    if shape == "c2q6":
+        st = runs[("0", False)]["meta"]["lpc_tiers"].astype(np.int64)
+        listed = np.nonzero(st >> 8 == 1)[0]
+        assert (listed < R).any() and (listed >= R).any(), listed
+
+
 @pytest.mark.parametrize("q", [6, 7, 9, 15])
 def test_c2_shape_fast_kernel_and_retry_list(az, q):
     """config 2 shape at higher precisions: the fast S16 MFMA kernel takes the units inside
