@@ -2,6 +2,10 @@
  * (see device_common.h for the design notes). */
 #include <type_traits>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "device_common.h"
 
 namespace flacmi {
@@ -539,11 +543,20 @@ static const void* lpc_kernel_T(const LpcArgs& a) {
 int64_t lpc_units_per_round(const LpcArgs& a) {
     const void* f = a.L <= 4 ? lpc_kernel_T<4>(a) : a.L <= 8 ? lpc_kernel_T<8>(a) : a.L <= 12 ? lpc_kernel_T<12>(a)
                   : a.L <= 16 ? lpc_kernel_T<16>(a) : lpc_kernel_T<32>(a);
-    int dev = 0, cus = 0, nb = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    /* the occupancy query costs about a millisecond of host time: once per (device, kernel) */
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, int64_t> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(dev, f);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int cus = 0, nb = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 256, 0) != hipSuccess)
         return 0;
-    return (int64_t)nb * 256 * cus;
+    return cache[key] = (int64_t)nb * 256 * cus;
 }
 
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s) {
