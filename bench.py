@@ -43,7 +43,17 @@ CONFIGS = {
     # configs[4]: fixed-only (-l 0 mode of this build) + Rice search
     "c5": dict(workload="fixed-only 4608-sample int16 blocks, -r 0,5",
                n=4608, bits=16, L=0, q=5, rmin=0, rmax=5, mode=1, units=1_000_000, channels=1),
+    # not a BASELINE config: FLAC's common 4096-sample block at -l 8 -r 0,4, which runs the
+    # runtime-shape kernel builds (the BASELINE shapes have constant-shape builds)
+    "b4096": dict(workload="1e6 synthetic mono 4096-sample int16 blocks, -l 8 -q 5 -r 0,4 (non-BASELINE shape)",
+                  n=4096, bits=16, L=8, q=5, rmin=0, rmax=4, mode=0, units=1_000_000, channels=1),
 }
+# --open K: K/8 of the units are MA(1) near-white noise (flacmi_synth_mix_device), whose LPC
+# candidates tie the fixed order-0 sum within a fraction of a percent, so neither the sign
+# bound nor the partial-sum tiers decide them and every candidate's exact sum is computed
+# (the reference's full candidate work, encoder.py:387-404, 537-548)
+OPEN_NOTE = ("open mix: {k}/8 of the units MA(1) near-white noise (LPC near-ties that no bound decides: every "
+             "candidate's exact sum), the rest the SURVEY §8d tones")
 METRIC = "PCM samples/sec encode-analysis, 4608-blk/16-bit mono, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
@@ -57,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--units", type=int, default=0, help="units per GPU (default: the config's); c4: chunk size")
     ap.add_argument("--total-units", type=int, default=0, help="c4: blocks in the whole job (default 1e8)")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--open", type=int, default=0, choices=range(9), metavar="K",
+                    help="K/8 of the units MA(1) near-white noise: the undecided-LPC workload (0 = the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--parity-units", type=int, default=64)
     ap.add_argument("--no-parity", action="store_true")
@@ -144,7 +156,7 @@ def _host_cpus():
     return model, nproc, usable
 
 
-def cpu_baseline(cfg, seconds, seed):
+def cpu_baseline(cfg, seconds, seed, open_eighths=0):
     """Oracle (oracle/flac_oracle.c, a C port of the reference's hot path) on host cores,
     on a bounded sample of the same workload (chunks of distinct synthetic units): every
     CPU this process may use, and one thread."""
@@ -160,7 +172,7 @@ def cpu_baseline(cfg, seconds, seed):
     def run(nthreads, budget, chunk, first):
         done, t_an = 0, 0.0
         while t_an < budget:
-            a = oracle.synth_batch(first + done, chunk, cfg["n"], cfg["bits"], seed, dtype=dt)
+            a = oracle.synth_batch(first + done, chunk, cfg["n"], cfg["bits"], seed, dtype=dt, open_eighths=open_eighths)
             t0 = time.perf_counter()
             oracle.analyze_batch(a, p, cfg["n"], sample_bits=cfg["bits"], threads=nthreads)
             t_an += time.perf_counter() - t0
@@ -197,7 +209,8 @@ def end_to_end_leg(args, cfg, az):
     stride = unit_stride(n, 2 if bits <= 16 else 4)
     dev = torch.device("cuda", torch.cuda.current_device())
     g = torch.empty((units, stride), dtype=dt, device=dev)
-    az.synth_device(g.data_ptr(), g.element_size(), bits, stride, 10_000_000, units, n, args.seed)
+    az.synth_device(g.data_ptr(), g.element_size(), bits, stride, 10_000_000, units, n, args.seed,
+                    open_eighths=args.open)
     torch.cuda.synchronize(dev)
     host = g.cpu().numpy()
     del g
@@ -442,7 +455,7 @@ def shard_plan(cfg, rank, world, units, total_units_arg=0):
     return 0, list(range(rank, n_chunks, world)), total
 
 
-def run_chunks(az, cfg, params, bufs, chunk_ids, units, total_units, seed, stream=0, on_chunk=None):
+def run_chunks(az, cfg, params, bufs, chunk_ids, units, total_units, seed, stream=0, on_chunk=None, open_eighths=0):
     """One rank's share of a chunked job (config 4): for each of its round-robin chunks,
     generate the chunk's blocks on the device (global block index = chunk * units + i, the
     frame number of the reference's block loop, encoder.py:87-97), analyse them and add the
@@ -455,7 +468,7 @@ def run_chunks(az, cfg, params, bufs, chunk_ids, units, total_units, seed, strea
     bufs["stats_acc"].zero_()
     for ci in chunk_ids:
         cu = min(units, total_units - ci * units)
-        az.synth_device(samples.data_ptr(), sbytes, bits, sstride, ci * units, cu, n, seed, stream)
+        az.synth_device(samples.data_ptr(), sbytes, bits, sstride, ci * units, cu, n, seed, stream, open_eighths)
         az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, cu, n, params, meta.data_ptr(),
                           rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, stream)
         az.stream_stats(meta.data_ptr(), cu, n, bufs["stats"].data_ptr(), stream)
@@ -511,6 +524,8 @@ def main(argv=None):
     if rc is not None:
         return rc
     cfg = dict(CONFIGS[args.config])
+    if args.open:
+        cfg["workload"] += "; " + OPEN_NOTE.format(k=args.open)
     units = args.units or cfg["units"]
     if args.launch_check:
         launch_check(args, cfg, units)
@@ -533,7 +548,7 @@ def main(argv=None):
     torch.cuda.set_device(dev)
 
     from flac_amd import abi
-    from flac_amd.analysis import Analyzer, make_params, params_stride_for, unit_stride
+    from flac_amd.analysis import Analyzer, get_knob, knob, make_params, params_stride_for, unit_stride
 
     az = Analyzer(local)
     stream = torch.cuda.current_stream(dev)
@@ -552,7 +567,7 @@ def main(argv=None):
     rparams = torch.empty((units, pstride), dtype=torch.int32, device=dev)
     residual = torch.empty((units, rstride), dtype=torch.int32, device=dev)
     stats = torch.zeros(abi.STATS_WORDS, dtype=torch.int64, device=dev)
-    az.synth_device(samples.data_ptr(), sbytes, bits, sstride, first_unit, units, n, args.seed, sptr)
+    az.synth_device(samples.data_ptr(), sbytes, bits, sstride, first_unit, units, n, args.seed, sptr, args.open)
     params = make_params(cfg["L"], cfg["q"], cfg["rmin"], cfg["rmax"], cfg["mode"])
 
     stats_acc = torch.zeros_like(stats)
@@ -567,7 +582,7 @@ def main(argv=None):
             az.stream_stats(meta.data_ptr(), units, n, stats.data_ptr(), sptr)
             reduce_stats(stats, dist, comm, sptr)
             return
-        run_chunks(az, cfg, params, bufs, my_chunks, units, total_units, args.seed, sptr)
+        run_chunks(az, cfg, params, bufs, my_chunks, units, total_units, args.seed, sptr, open_eighths=args.open)
         reduce_stats(stats_acc, dist, comm, sptr)
         stats.copy_(stats_acc)
 
@@ -604,15 +619,13 @@ def main(argv=None):
     kt = az.timing()
     elapsed = reduce_elapsed(elapsed, dist, dev)
     kt_steps, isolated_calls = kt, 0
-    if cfg["L"] > 0 and not cfg["mode"] and os.environ.get("FLACMI_OVERLAP", "") != "0":
+    if cfg["L"] > 0 and not cfg["mode"] and get_knob("FLACMI_OVERLAP") != 0:
         # The library's default chunking overlaps k_lpc's last, partly filled round with
         # k_resid of the first chunk (flacmi_host.cpp overlap_mode), so the timed
         # steps' stage spans include the other kernel's waves.  The roofline prices each kernel
-        # on launches of its own: a few more calls with one chunk (FLACMI_OVERLAP=0, read per
-        # call), after the timed region.
-        prev = os.environ.get("FLACMI_OVERLAP")
-        os.environ["FLACMI_OVERLAP"] = "0"
-        try:
+        # on launches of its own: a few more calls with one chunk (the FLACMI_OVERLAP knob at 0),
+        # after the timed region.
+        with knob("FLACMI_OVERLAP", 0):
             step()
             torch.cuda.synchronize(dev)
             az.timing_reset()
@@ -621,11 +634,6 @@ def main(argv=None):
                 step()
             torch.cuda.synchronize(dev)
             kt = az.timing()
-        finally:
-            if prev is None:
-                del os.environ["FLACMI_OVERLAP"]
-            else:
-                os.environ["FLACMI_OVERLAP"] = prev
 
     meta_np = meta.cpu().numpy().view(abi.META_DTYPE).reshape(units)
     st = stats.cpu().numpy()
@@ -684,7 +692,8 @@ def main(argv=None):
     dom_bytes = resid_b if dominant == "k_resid" else lpc_b
     dom_ms = kt["resid_ms"] if dominant == "k_resid" else kt["lpc_ms"]
     traffic, traffic_lib = None, None
-    tfile = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
+    tfile = os.path.join(REPO, "profiles", f"traffic_{args.config}" + (f"_open{args.open}" if args.open else "") +
+                         ("_noprune" if os.environ.get("FLACMI_NO_PRUNE", "0") not in ("", "0") else "") + ".json")
     if os.path.exists(tfile):  # HBM bytes per launch from the separate rocprofv3 --pmc passes
         try:
             tj = json.load(open(tfile))
@@ -701,7 +710,7 @@ def main(argv=None):
 
     if rank == 0:
         # rank 0 only, after the timed region (the other ranks are idle by then)
-        cpu = cpu_baseline(cfg, args.cpu_seconds, args.seed) if args.cpu_seconds > 0 else None
+        cpu = cpu_baseline(cfg, args.cpu_seconds, args.seed, args.open) if args.cpu_seconds > 0 else None
         line = {
             "metric": METRIC,
             "value": value,
@@ -714,11 +723,16 @@ def main(argv=None):
             "scaling": "strong" if chunked else "weak",
             "vs_baseline": None,
             "dtype": "i16 in; f64 autocorrelation/Levinson; i32 predictors",
-            "data": "synthetic: on-device integer generator (3 DDS tones + splitmix64 noise, SURVEY §8d)",
+            "data": "synthetic: on-device integer generator (3 DDS tones + splitmix64 noise, SURVEY §8d)" +
+                    (f"; {args.open}/8 of the units MA(1) near-white noise (--open)" if args.open else ""),
             "config": {"workload": cfg["workload"], "units_per_gpu": total_units // world,
                        "units_total": total_units, "chunk_units": units if chunked else None, "block": n, "sample_bits": bits,
                        "max_lpc_order": cfg["L"], "qlp_precision": cfg["q"], "rice": [cfg["rmin"], cfg["rmax"]],
                        "mode": "fixed-only" if cfg["mode"] else "reference", "parallelism": f"dp{world} (block shards)",
+                       "open_eighths": args.open,
+                       "lpc_pruning": ("off: every LPC candidate's exact sum (FLACMI_NO_PRUNE=1)"
+                                       if os.environ.get("FLACMI_NO_PRUNE", "0") not in ("", "0") else
+                                       "on: candidates proven to lose skipped (sign bound, partial-sum tiers)"),
                        "stats_collective": ("flacmi_allreduce_stats (C-ABI, RCCL)" if comm is not None else
                                             f"torch.distributed all_reduce ({comm_note})" if distributed else None)},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": dom_gbs, "peak": HBM_PEAK_GBS,

@@ -235,6 +235,8 @@ SIGNATURES = {
     "flacmi_comm_destroy": (C.c_int, [C.c_void_p]),
     "flacmi_synth_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,
                                       C.c_int64, C.c_int64, C.c_int32, C.c_uint64, C.c_void_p]),
+    "flacmi_synth_mix_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,
+                                          C.c_int64, C.c_int64, C.c_int32, C.c_uint64, C.c_int32, C.c_void_p]),
     "flacmi_device_alloc": (C.c_void_p, [C.c_void_p, C.c_size_t]),
     "flacmi_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "flacmi_memcpy_h2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
@@ -242,6 +244,8 @@ SIGNATURES = {
     "flacmi_synchronize": (C.c_int, [C.c_void_p]),
     "flacmi_last_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int]),
     "flacmi_timing_reset": (C.c_int, [C.c_void_p]),
+    "flacmi_set_knob": (C.c_int, [C.c_char_p, C.c_int32]),
+    "flacmi_get_knob": (C.c_int, [C.c_char_p, C.POINTER(C.c_int32)]),
     "flacmi_host_pypow2": (C.c_double, [C.c_double, C.POINTER(C.c_int32)]),
     "flacmi_host_floor_log2": (C.c_int32, [C.c_double]),
     "flacmi_device_selftest": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,

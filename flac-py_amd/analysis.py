@@ -63,6 +63,36 @@ def unit_stride(block_len: int, sample_bytes: int) -> int:
     return v
 
 
+def get_knob(name: str) -> int:
+    """A test/diagnostic knob of the library (flacmi_get_knob)."""
+    v = C.c_int32(0)
+    check(load().flacmi_get_knob(name.encode(), C.byref(v)), "flacmi_get_knob")
+    return v.value
+
+
+def set_knob(name: str, value: int) -> None:
+    """Set a test/diagnostic knob (flacmi_set_knob): FLACMI_OVERLAP, FLACMI_MF8_GRID,
+    FLACMI_STREAM_GENERIC.  The library reads their environment variables once; this is the
+    thread-safe way to change them afterwards."""
+    check(load().flacmi_set_knob(name.encode(), int(value)), "flacmi_set_knob")
+
+
+class knob:
+    """`with knob("FLACMI_OVERLAP", 0): ...` sets a knob and restores its previous value."""
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.prev = get_knob(self.name)
+        set_knob(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_knob(self.name, self.prev)
+        return False
+
+
 def params_stride_for(rice_max: int) -> int:
     return (1 << max(rice_max, 0)) + 1
 
@@ -353,13 +383,16 @@ class Analyzer:
         check(self.lib.flacmi_timing_reset(self.ctx), "flacmi_timing_reset")
 
     def synth_device(self, dst_ptr: int, sample_bytes: int, sample_bits: int, unit_stride: int,
-                     first_unit: int, n_units: int, length: int, seed: int, stream: int = 0) -> None:
+                     first_unit: int, n_units: int, length: int, seed: int, stream: int = 0,
+                     open_eighths: int = 0) -> None:
+        """Synthetic units on the device (flacmi_synth_mix_device; open_eighths / 8 of them the
+        "open" mix's near-white noise)."""
         done = 0
         while done < n_units:
             k = min(1 << 30, n_units - done)
-            check(self.lib.flacmi_synth_device(self.ctx, dst_ptr + done * unit_stride * sample_bytes,
-                                               sample_bytes, sample_bits, unit_stride, first_unit + done,
-                                               k, length, seed, stream), "flacmi_synth_device")
+            check(self.lib.flacmi_synth_mix_device(self.ctx, dst_ptr + done * unit_stride * sample_bytes,
+                                                   sample_bytes, sample_bits, unit_stride, first_unit + done,
+                                                   k, length, seed, open_eighths, stream), "flacmi_synth_mix_device")
             done += k
 
     def stream_stats(self, meta_ptr: int, n_units: int, block_len: int, stats_ptr: int,

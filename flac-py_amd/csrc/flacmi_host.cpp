@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <chrono>
 #include <cmath>
@@ -169,12 +170,13 @@ struct flacmi_ctx {
     /* per call: start, LPC done, residual done, then (overlap) per chunk the k_resid start/end */
     hipEvent_t ev[kRing][3 + 2 * kMaxChunks] = {};
     int nchunks[kRing] = {};
-    hipStream_t side = nullptr;          /* k_lpc stream of the overlap mode */
     hipEvent_t lpc_done[kMaxChunks] = {}; /* k_lpc of chunk i finished (no timing) */
     int ncalls = 0; /* calls since the last timing reset */
     struct EncState* enc = nullptr; /* flacmi_encode_pipeline's streams, slots and pinned arrays */
 };
 static void enc_free(struct EncState* es);
+static int enc_streams(flacmi_ctx* ctx);
+static hipStream_t enc_side(flacmi_ctx* ctx);
 
 static int ensure_buf(DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return 0;
@@ -200,7 +202,52 @@ static int set_device(flacmi_ctx* ctx) {
     return 0;
 }
 
+/* flacmi_set_knob: environment read once, then atomics (no getenv on launch paths) */
+namespace {
+struct KnobDef {
+    const char* name;
+    int dflt;
+};
+constexpr KnobDef kKnobs[kKnobCount] = {{"FLACMI_OVERLAP", -1}, {"FLACMI_MF8_GRID", 0}, {"FLACMI_STREAM_GENERIC", 0}};
+std::atomic<int> g_knob[kKnobCount];
+std::once_flag g_knob_once;
+void knobs_init() {
+    std::call_once(g_knob_once, [] {
+        for (int i = 0; i < kKnobCount; ++i) {
+            const char* e = getenv(kKnobs[i].name);
+            g_knob[i].store(e && e[0] ? atoi(e) : kKnobs[i].dflt);
+        }
+    });
+}
+int knob_index(const char* name) {
+    if (!name) return -1;
+    for (int i = 0; i < kKnobCount; ++i)
+        if (strcmp(name, kKnobs[i].name) == 0) return i;
+    return -1;
+}
+}  // namespace
+
+int flacmi::knob(Knob k) {
+    knobs_init();
+    return g_knob[k].load(std::memory_order_relaxed);
+}
+
 extern "C" {
+
+int flacmi_set_knob(const char* name, int32_t value) {
+    const int i = knob_index(name);
+    if (i < 0) return fail(FLACMI_E_INVALID, "unknown knob %s", name ? name : "(null)");
+    knobs_init();
+    g_knob[i].store(value);
+    return 0;
+}
+
+int flacmi_get_knob(const char* name, int32_t* value) {
+    const int i = knob_index(name);
+    if (i < 0 || !value) return fail(FLACMI_E_INVALID, "unknown knob %s", name ? name : "(null)");
+    *value = knob((Knob)i);
+    return 0;
+}
 
 int flacmi_abi_version(void) { return FLACMI_ABI_VERSION; }
 
@@ -272,7 +319,6 @@ void flacmi_destroy(flacmi_ctx* ctx) {
         for (auto& ev : slot)
             if (ev) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     for (auto& ev : ctx->lpc_done)
         if (ev) (void)hipEventDestroy(ev);
     delete ctx;
@@ -439,19 +485,16 @@ static int prune_allowed() {
 }
 
 /* k_lpc and k_resid of consecutive chunks overlap on two streams (see analyze_device_impl).
- * FLACMI_OVERLAP (read per call): unset or -1 = round-aligned (the default): the units of
+ * FLACMI_OVERLAP (flacmi_set_knob; the environment's value at first use): unset or -1 = round-aligned (the default): the units of
  * k_lpc's whole rounds, then the remainder (a partly filled last round), whose k_lpc runs
  * beside k_resid of the first chunk, when the remainder holds at least kOverlapMinUnits;
  * 0 = no overlap; k > 1 = up to k equal chunks of at least kOverlapMinUnits; -R (R > 1) =
  * round-aligned with R units per round and no minimum (tests). */
 constexpr int64_t kOverlapMinUnits = 16384;
-static int overlap_mode() {
-    const char* e = getenv("FLACMI_OVERLAP");
-    return e && e[0] ? atoi(e) : -1;
-}
+static int overlap_mode() { return knob(kKnobOverlap); }
 
 static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const flacmi_params* p,
-                               const flacmi_outputs* o, hipStream_t s) {
+                               const flacmi_outputs* o, hipStream_t s, bool allow_overlap = true) {
     if (int rc = set_device(ctx)) return rc;
     const bool lpc = p->mode == FLACMI_MODE_REFERENCE || p->mode == FLACMI_MODE_LPC_ONLY;
     const int L = lpc ? p->max_lpc_order : 0;
@@ -460,8 +503,9 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         if (int rc = ensure_buf(ctx->rec, sizeof(int32_t) * (size_t)rec_words * (size_t)(b->n_units > 0 ? b->n_units : 1)))
             return rc;
     }
-    /* fast-kernel retry list: a counter, then one batch index per unit */
-    if (int rc = ensure_buf(ctx->retry, sizeof(int64_t) * (size_t)(b->n_units + 2))) return rc;
+    /* fast-kernel retry lists: a counter, then one batch index per unit (k_resid_stream's list
+     * kernel hands units on through a second one behind it) */
+    if (int rc = ensure_buf(ctx->retry, sizeof(int64_t) * (size_t)(2 * b->n_units + 4))) return rc;
     struct Cls {
         int64_t unit0, count;
         int n;
@@ -566,6 +610,8 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.mfma = use_mfma();
         a.retry_count = (unsigned long long*)ctx->retry.p;
         a.retry_list = (int64_t*)ctx->retry.p + 2;
+        a.retry2_count = (unsigned long long*)((int64_t*)ctx->retry.p + 2 + b->n_units);
+        a.retry2_list = (int64_t*)ctx->retry.p + 4 + b->n_units;
         a.sample_bits = b->sample_bits;
         a.stream = use_stream();
         a.prune = p->mode == FLACMI_MODE_REFERENCE && !o->lpc_sums && !(p->reserved[1] & FLACMI_FLAG_ALL_CANDIDATES) &&
@@ -578,30 +624,35 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
     };
     const int slot = ctx->ncalls % flacmi_ctx::kRing;
     hipEvent_t* ev = ctx->ev[slot];
+    hipStream_t side = nullptr;
+    if (overlap && !allow_overlap) overlap = false;
+    if (overlap) {
+        /* k_lpc runs on the pipeline's H2D stream, which lives as long as the context: a
+         * stream created here would have to be destroyed before returning, and destroying a
+         * stream with queued work waits for it (the call would block the host).  A stream
+         * left open instead takes a hardware queue that the pipeline's copies then share
+         * (measured: the 1e5-unit host-to-host encode 20.4 -> 38.5 ms wall). */
+        if (int rc = enc_streams(ctx)) return rc;
+        side = enc_side(ctx);
+        if (side == s) overlap = false;
+    }
     ctx->nchunks[slot] = overlap ? nch : 0;
     HIP_TRY(hipEventRecord(ev[0], s));
     if (overlap) {
-        if (!ctx->side) HIP_TRY(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-        HIP_TRY(hipStreamWaitEvent(ctx->side, ev[0], 0));
+        HIP_TRY(hipStreamWaitEvent(side, ev[0], 0));
         for (int i = 0; i < nch; ++i) {
             LpcArgs a;
             if (int rc = lpc_args(ch[i], a)) return rc;
-            HIP_TRY(launch_lpc(a, ctx->side));
-            HIP_TRY(hipEventRecord(ctx->lpc_done[i], ctx->side));
+            HIP_TRY(launch_lpc(a, side));
+            HIP_TRY(hipEventRecord(ctx->lpc_done[i], side));
         }
-        HIP_TRY(hipEventRecord(ev[1], ctx->side));
+        HIP_TRY(hipEventRecord(ev[1], side));
         for (int i = 0; i < nch; ++i) {
             HIP_TRY(hipStreamWaitEvent(s, ctx->lpc_done[i], 0));
             HIP_TRY(hipEventRecord(ev[3 + 2 * i], s));
             HIP_TRY(launch_resid_chunk(ch[i], s));
             HIP_TRY(hipEventRecord(ev[4 + 2 * i], s));
         }
-        /* The side stream lives for this call only.  A process holds GPU_MAX_HW_QUEUES (4)
-         * hardware queues; a lingering extra stream shares one of them with the streams a
-         * later encode pipeline creates, and its copies and kernels then serialise (measured:
-         * the 1e5-unit host-to-host encode 20.4 -> 38.5 ms wall). */
-        HIP_TRY(hipStreamDestroy(ctx->side));
-        ctx->side = nullptr;
     } else {
         for (int i = 0; i < nch && lpc; ++i) {
             LpcArgs a;
@@ -957,6 +1008,8 @@ struct EncState {
     int64_t cap_nf = 0; /* frames the pinned arrays of each slot hold */
 };
 
+static hipStream_t enc_side(flacmi_ctx* ctx) { return ctx->enc ? ctx->enc->is : nullptr; }
+
 static void enc_free(EncState* es) {
     if (!es) return;
     for (hipStream_t st : {es->is, es->os})
@@ -974,7 +1027,10 @@ static void enc_free(EncState* es) {
     delete es;
 }
 
-static int enc_state(flacmi_ctx* ctx, int64_t per_nf, EncState** out) {
+/* The pipeline's streams, created on first use and kept for the context's lifetime.  The
+ * overlap mode of analyze_device_impl borrows `is` for its k_lpc launches, so no call creates
+ * or destroys a stream of its own (a process holds GPU_MAX_HW_QUEUES hardware queues). */
+static int enc_streams(flacmi_ctx* ctx) {
     if (!ctx->enc) {
         /* built whole before it is published: a failed create leaves no half state behind */
         EncState* es = new EncState();
@@ -989,6 +1045,11 @@ static int enc_state(flacmi_ctx* ctx, int64_t per_nf, EncState** out) {
         }
         ctx->enc = es;
     }
+    return 0;
+}
+
+static int enc_state(flacmi_ctx* ctx, int64_t per_nf, EncState** out) {
+    if (int rc = enc_streams(ctx)) return rc;
     EncState* es = ctx->enc;
     if (es->cap_nf < per_nf) {
         for (auto& sl : es->slot) {
@@ -1049,7 +1110,9 @@ static int enc_front(flacmi_ctx* ctx, EncSlot& sl, const flacmi_batch* whole, co
     o.residual_bytes = sl.rbytes;
     o.residual_stride = rstride;
     if (int rc = validate(&db, params, &o)) return rc;
-    if (int rc = analyze_device_impl(ctx, &db, params, &o, cs)) return rc;
+    /* no chunk overlap inside the pipeline: its side stream is this pipeline's H2D stream,
+       and the next sub-batch's copy would queue behind this one's k_lpc */
+    if (int rc = analyze_device_impl(ctx, &db, params, &o, cs, false)) return rc;
     HIP_TRY(hipEventRecord(sl.e[2], cs));
     flacmi_frame_params f = *fp;
     f.first_frame = fp->first_frame + sl.first_unit / fp->channels;
@@ -1373,18 +1436,26 @@ int flacmi_comm_destroy(flacmi_comm* comm) {
     return rc;
 }
 
-int flacmi_synth_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_t sample_bits, int64_t unit_stride,
-                        int64_t first_unit, int64_t n_units, int32_t len, uint64_t seed, void* stream) {
+int flacmi_synth_mix_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_t sample_bits,
+                            int64_t unit_stride, int64_t first_unit, int64_t n_units, int32_t len, uint64_t seed,
+                            int32_t open_eighths, void* stream) {
     if (!ctx || !dst) return fail(FLACMI_E_INVALID, "null argument");
     if (sample_bytes != 2 && sample_bytes != 4) return fail(FLACMI_E_INVALID, "sample_bytes must be 2 or 4");
     if (sample_bits < 8 || sample_bits > 8 * sample_bytes || (sample_bits > 16 && sample_bits - 16 > 15))
         return fail(FLACMI_E_INVALID, "sample_bits out of range");
     if (len < 1 || unit_stride < len) return fail(FLACMI_E_INVALID, "bad length/stride");
     if (n_units > 0x7fffffff) return fail(FLACMI_E_INVALID, "at most 2^31-1 units per synth call");
+    if (open_eighths < 0 || open_eighths > 8) return fail(FLACMI_E_INVALID, "open_eighths must be 0..8");
     if (int rc = set_device(ctx)) return rc;
     HIP_TRY(launch_synth(dst, sample_bytes, sample_bits, unit_stride, first_unit, n_units, len, seed, ctx->d_sintab,
-                         (hipStream_t)stream));
+                         open_eighths, (hipStream_t)stream));
     return 0;
+}
+
+int flacmi_synth_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_t sample_bits, int64_t unit_stride,
+                        int64_t first_unit, int64_t n_units, int32_t len, uint64_t seed, void* stream) {
+    return flacmi_synth_mix_device(ctx, dst, sample_bytes, sample_bits, unit_stride, first_unit, n_units, len, seed, 0,
+                                   stream);
 }
 
 void* flacmi_device_alloc(flacmi_ctx* ctx, size_t bytes) {

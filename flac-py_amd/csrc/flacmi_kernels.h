@@ -54,6 +54,8 @@ struct ResidArgs {
     int32_t mfma;            /* 1 = MFMA candidate sums where exact (env FLACMI_NO_MFMA=1 -> 0) */
     unsigned long long* retry_count; /* fast-path units handed to the generic kernel: count, */
     int64_t* retry_list;             /* and their batch indices (NULL: no fast path) */
+    unsigned long long* retry2_count; /* k_resid_stream: the units its list kernel hands on to k_resid's */
+    int64_t* retry2_list;             /* list variant (a second list of at most count entries) */
     int32_t sample_bits;             /* declared sample width (bounds the 64-bit paths' narrow sums) */
     int32_t stream;                  /* 1 = k_resid_stream where the shape allows (env FLACMI_NO_STREAM=1 -> 0) */
     int32_t prune;                   /* 1 = reference mode may skip the exact LPC candidate sums of a unit
@@ -127,6 +129,10 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes);
 /* Largest partition order the LDS tables support. */
 constexpr int kMaxFinestParts = 4096;
 
+/* flacmi_set_knob's knobs: the environment's value (read once) or the last value set */
+enum Knob { kKnobOverlap = 0, kKnobMf8Grid, kKnobStreamGeneric, kKnobCount };
+int knob(Knob k);
+
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);
 /* units one full round of launch_lpc's kernel covers on the current device (resident
  * workgroups per CU x 256 units x CUs); 0 when the occupancy query fails */
@@ -144,7 +150,7 @@ hipError_t launch_expand_records(const int32_t* rec, int32_t rec_words, int32_t 
                                  int32_t* out, hipStream_t s);
 hipError_t launch_synth(void* dst, int32_t sample_bytes, int32_t bits, int64_t stride,
                         int64_t first_unit, int64_t n_units, int32_t len, uint64_t seed,
-                        const int32_t* sintab, hipStream_t s);
+                        const int32_t* sintab, int32_t open8, hipStream_t s);
 hipError_t launch_stats(const flacmi_unit_meta* meta, int64_t n_units, int32_t block_len,
                         int32_t tail_len, int64_t n_tail_units, int64_t* stats, hipStream_t s);
 

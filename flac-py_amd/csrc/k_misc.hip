@@ -39,13 +39,44 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-/* SURVEY §8d synthetic signal; identical integer recipe to oracle_synth_unit. */
+__device__ __forceinline__ int32_t synth_bsum(uint64_t r) { return (int32_t)__builtin_amdgcn_sad_u8((uint32_t)r, 0u, 0u); }
+
+/* a 16-bit value to `bits` bits (low random bits from the sample's hash when widening), clipped */
+__device__ __forceinline__ int64_t synth_widen(int64_t v, uint64_t r, int32_t bits) {
+    const int64_t lo = -(1LL << (bits - 1)), hi = (1LL << (bits - 1)) - 1;
+    if (bits > 16) {
+        const int e = bits - 16;
+        v = v * (1LL << e) + (int64_t)((r >> 32) & ((1ull << e) - 1)) - (1LL << (e - 1));
+    } else if (bits < 16) {
+        v >>= (16 - bits);
+    }
+    return v < lo ? lo : (v > hi ? hi : v);
+}
+
+/* SURVEY §8d synthetic signal; identical integer recipe to oracle_synth_unit.  open8 > 0: a
+ * unit whose hash byte (h0 >> 56) & 7 is below open8 is the "open" mix's MA(1) near-white
+ * noise instead (oracle_synth_unit_mix): LPC candidates the sign bound cannot decide. */
 template <typename T>
 __global__ __launch_bounds__(256) void k_synth(T* dst, int32_t bits, int64_t stride, int64_t first_unit,
-                                               int32_t len, uint64_t seed, const int32_t* __restrict__ sintab) {
+                                               int32_t len, uint64_t seed, const int32_t* __restrict__ sintab,
+                                               int32_t open8) {
     const int64_t uu = blockIdx.x;
     const int64_t unit = first_unit + uu;
     const uint64_t h0 = splitmix64(seed ^ ((uint64_t)unit * 0xD1B54A32D192ED03ull));
+    if ((int32_t)((h0 >> 56) & 7) < open8) {
+        /* |w| <= 510 * 4095 / 128 < 2^14: the products are exact 24-bit multiplies */
+        const int32_t sg = 1024 + (int32_t)(splitmix64(h0 + 5) % 3072);
+        const int32_t ma = (int32_t)(splitmix64(h0 + 6) % 7) - 3;
+        const uint64_t base = seed ^ ((uint64_t)unit << 32);
+        for (int i = threadIdx.x; i < len; i += 256) {
+            const uint64_t r = splitmix64(base ^ (uint64_t)i);
+            const uint64_t rp = splitmix64(base ^ (uint64_t)(int64_t)(i - 1));
+            const int32_t w = __mul24(synth_bsum(r) - 510, sg) >> 7;
+            const int32_t wp = __mul24(synth_bsum(rp) - 510, sg) >> 7;
+            dst[uu * stride + i] = (T)synth_widen((int64_t)(w + ((ma * wp) >> 7)), r, bits);
+        }
+        return;
+    }
     int64_t amp[3];
     uint32_t dphi[3], phi0[3];
 #pragma unroll
@@ -249,15 +280,18 @@ hipError_t launch_expand_records(const int32_t* rec, int32_t rec_words, int32_t 
 }
 
 hipError_t launch_synth(void* dst, int32_t sample_bytes, int32_t bits, int64_t stride, int64_t first_unit,
-                        int64_t n_units, int32_t len, uint64_t seed, const int32_t* sintab, hipStream_t s) {
+                        int64_t n_units, int32_t len, uint64_t seed, const int32_t* sintab, int32_t open8,
+                        hipStream_t s) {
     if (n_units <= 0) return hipSuccess;
     /* one workgroup per unit: the per-unit recipe (64-bit splitmix, divisions) is scalar
      * work each wave repeats, so every thread loops over len / 256 samples */
     const dim3 grid((unsigned)n_units);
     if (sample_bytes == 2)
-        hipLaunchKernelGGL(k_synth<int16_t>, grid, dim3(256), 0, s, (int16_t*)dst, bits, stride, first_unit, len, seed, sintab);
+        hipLaunchKernelGGL(k_synth<int16_t>, grid, dim3(256), 0, s, (int16_t*)dst, bits, stride, first_unit, len, seed, sintab,
+                           open8);
     else
-        hipLaunchKernelGGL(k_synth<int32_t>, grid, dim3(256), 0, s, (int32_t*)dst, bits, stride, first_unit, len, seed, sintab);
+        hipLaunchKernelGGL(k_synth<int32_t>, grid, dim3(256), 0, s, (int32_t*)dst, bits, stride, first_unit, len, seed, sintab,
+                           open8);
     return hipGetLastError();
 }
 

@@ -2706,13 +2706,10 @@ static inline int device_cus() {
         ncu = 256;
     return ncu;
 }
-/* FLACMI_MF8_GRID=k (test knob, read per launch): at most k workgroups in kVarMf8's persistent
+/* FLACMI_MF8_GRID=k (test knob, flacmi_set_knob): at most k workgroups in kVarMf8's persistent
  * grid and in the 64-bit list variant's, so each loops over many units (kVarMf8's next-unit
  * prefetch path, kVarList1's unit loop) */
-static inline int mf8_grid_cap() {
-    const char* e = getenv("FLACMI_MF8_GRID");
-    return e ? atoi(e) : 0;
-}
+static inline int mf8_grid_cap() { return knob(kKnobMf8Grid); }
 
 /* S16 MFMA fast kernel over the batch, then the generic body over the units it listed */
 template <int LMAX>
@@ -2834,9 +2831,13 @@ __host__ __device__ inline int sb_finest_order(int n, int rmin, int rmax) {
 }
 
 /* k_resid_sb's shapes: 8192 <= n <= 16384 (n % 256 == 0: at most four chunks per thread),
- * finest Rice order 6..8 with a power-of-two number of whole chunks per partition */
+ * finest Rice order 6..8 with a power-of-two number of whole chunks per partition.  Samples of
+ * at most 24 bits: the kernel lists a unit only when |x| > 2^23, and its 32-bit K_j row sums
+ * assume every term in [-2^23, 2^23 - 1] (x = +2^23 needs 25 bits).  k_resid_sb writes no
+ * fixed_sums rows, so a caller asking for them takes kVarMf8, which does. */
 static inline bool sb_shape_ok(const ResidArgs& a) {
     if (a.n < 8192 || a.n > 16384 || a.n % 256 != 0) return false;
+    if (a.sample_bits > 24 || a.fixed_sums) return false;
     const int om = sb_finest_order(a.n, a.rmin, a.rmax);
     if (om < 6 || om > 8) return false;
     const int ps = a.n >> om, cpp = ps >> 3;

@@ -306,17 +306,24 @@ __device__ __forceinline__ void store_meta(flacmi_unit_meta* m, int lane, const 
 
 }  // namespace
 
-/* NG = number of LPC MFMA groups (ceil(L / 4)), 0 in fixed-only mode.  R05: the Rice
- * partition orders are 0..5 for every unit (host-checked: rmin 0, n % 32 == 0 and n / 32 >
- * every predictor order), so the order loops compile without per-order branches.  One
- * workgroup per unit; every exit is workgroup-uniform (all waves decide from the same LDS
- * data). */
-template <int NG, bool R05, int NFIX = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7, 8))) void k_resid_stream(ResidArgs a) {
-    extern __shared__ __align__(16) unsigned char smem[];
+/* One unit (batch index gid) through the whole analysis.  NG = number of LPC MFMA groups
+ * (ceil(L / 4)), 0 in fixed-only mode.  R05: the Rice partition orders are 0..5 for every
+ * unit (host-checked: rmin 0, n % 32 == 0 and n / 32 > every predictor order), so the order
+ * loops compile without per-order branches.  Every exit is workgroup-uniform (all waves decide
+ * from the same LDS data).
+ * LIST (k_resid_stream_list, the units the batch kernel listed): the LPC groups' B operands
+ * drop the x tap T_p[0] = -2^shift, so the MFMA result is M + pred, exact while sum|c| <= 127
+ * whatever the shift; every LPC value is then exact, |r| = |x - floor(pred / 2^shift)| by a
+ * shift, a subtract and one v_sad_u32 (no pruning tiers: the units a large shift lists are
+ * mostly near-ties no bound decides).  A unit outside even that bound goes to the second list
+ * (k_resid's list variant). */
+template <int NG, bool R05, int NFIX, bool LIST, typename Args>
+__device__ __forceinline__ void stream_unit(const Args& a, const int64_t gid, unsigned char* smem) {
     /* NFIX: the block length (and L = 4 NG, the workgroup size) as compile-time constants, the
      * BASELINE configs' 4608-sample units: loop bounds, chunk guards and partition indices fold */
-    const int tid = threadIdx.x, NT = NFIX ? stream_threads(NFIX) : (int)blockDim.x, lane = tid & 63, nw = NT >> 6;
+    /* LIST: the thread id through an opaque register per unit (hoisted out of the unit loop,
+     * every value derived from it would stay live across the whole body) */
+    const int tid = LIST ? (int)opaque((uint32_t)threadIdx.x) : (int)threadIdx.x, NT = NFIX ? stream_threads(NFIX) : (int)blockDim.x, lane = tid & 63, nw = NT >> 6;
 #if FLACMI_STREAM_STAMPS /* diagnostic build only: per-unit phase clock stamps of wave 0 */
     uint64_t stamp[8];
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
@@ -326,7 +333,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
 #define STAMP(k) ((void)0)
 #endif
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t gid = blockIdx.x;
     const int n = NFIX ? NFIX : a.n, L = NG > 0 ? (NFIX ? 4 * NG : a.L) : 0;
     const int nch = n >> 3, nblk = n >> 6;
     const int rw = NG > 0 ? (NFIX ? 2 + L + (L * (L + 1)) / 2 : a.rec_words) : 0;
@@ -447,7 +453,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
      * sum for every order, LPC loses strictly (encoder.py:135-157: no win, no tie) and its
      * exact sums are never needed.  Otherwise the LPC groups run again, exact, over every
      * block (a workgroup-uniform branch: every wave decides from the same LDS words). */
-    const bool prune = NG > 0 && a.prune;
+    const bool prune = NG > 0 && a.prune && !LIST;
     unsigned long long* red64 = reinterpret_cast<unsigned long long*>(smem + lay.red); /* [nw][4 groups][4 orders] */
     auto lane_total = [&]() __attribute__((always_inline)) -> uint64_t {
         /* lanes 1..4: fixed orders 1..4, lane 0: order 0 (sum|x|), lanes 16..15+4NG: LPC orders */
@@ -492,7 +498,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             } else {
                 const int p = 4 * (g - 1) + o4 + 1, wb = 10 * (p - 1) + (k0 >> 1);
                 const uint32_t w0 = tt[wb], w1 = tt[wb + 1], w2 = tt[wb + 2];
-                const uint32_t l0 = __builtin_amdgcn_alignbit(w1, w0, alb), l2 = __builtin_amdgcn_alignbit(w2, w1, alb);
+                uint32_t l0 = __builtin_amdgcn_alignbit(w1, w0, alb), l2 = __builtin_amdgcn_alignbit(w2, w1, alb);
+                if constexpr (LIST) {
+                    /* pred-only taps: T_p[0] = -2^shift is half rho of (l0, l2) on the kb = 3 lanes
+                     * (their window is T[rho] .. T[rho - 3]); the table keeps it (the shift is read
+                     * from it below) */
+                    const uint32_t keep = kb == 3 ? ((rho & 1) ? 0x0000ffffu : 0xffff0000u) : 0xffffffffu;
+                    l0 &= rho < 2 ? keep : 0xffffffffu;
+                    l2 &= rho >= 2 ? keep : 0xffffffffu;
+                }
                 const h2 k256{(_Float16)256.0f, (_Float16)256.0f};
                 const uint32_t h0 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, l0) * k256);
                 const uint32_t hh = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, l2) * k256);
@@ -510,11 +524,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             }
             shg[g] = sh;
         }
-        if (NG > 0 && __ballot(outside)) { /* outside the MFMA exactness bound: k_resid redoes it */
+        if (NG > 0 && __ballot(outside)) {
+            /* outside the MFMA exactness bound: the list kernel (pred-only taps) redoes it, and a
+             * unit outside that bound too goes to k_resid's list variant */
             if (tid == 0) {
                 meta->status = FLACMI_STATUS_RETRY;
-                const unsigned long long k = atomicAdd(a.retry_count, 1ull);
-                a.retry_list[k] = gid;
+                const unsigned long long k = atomicAdd(LIST ? a.retry2_count : a.retry_count, 1ull);
+                (LIST ? a.retry2_list : a.retry_list)[k] = gid;
             }
             return;
         }
@@ -539,9 +555,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             const uint32_t t = opaque((uint32_t)tid);
             return *reinterpret_cast<const uint2*>(xs + 4 * (int)(t & 15) - 12 + 4 * (int)((t >> 4) & 3));
         };
+        /* LIST: the samples of the lane's four values (block blk, rows 4 kb + r, phase rho), as
+         * x - 2^31 (mod 2^32) from the biased x + 2^15 */
+        auto ldx = [&](int blk, uint32_t (&xn)[4]) __attribute__((always_inline)) {
+            if constexpr (LIST) {
+                const uint16_t* xp = xs + 64 * blk + 16 * kb + rho;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xn[r] = (uint32_t)xp[4 * r] + 0x7FFF8000u;
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xn[r] = 0u;
+            }
+        };
+        /* an exact LPC value's |r|: floor(T / 2^s) = (bits >> s) - (M >> s) with the x tap in B;
+         * LIST: (bits >> s) - (M >> s) = floor(pred / 2^s), and (bits >> s) - (x - 2^31) =
+         * (M >> s) - r + 2^31, so |r| is one v_sad_u32 against (M >> s) + 2^31 */
+        auto lpc_abs = [&](uint32_t bits, int sh, uint32_t kgv, uint32_t xn, uint32_t acc) __attribute__((always_inline)) {
+            return LIST ? sad32((bits >> sh) - xn, kgv + 0x80000000u, acc) : sad32(bits >> sh, kgv, acc);
+        };
         /* one 64-sample block through the MFMAs of groups G0..G1; EX: LPC values exact, else
          * the bound |T| */
-        auto blockA = [&](auto g0c, auto g1c, auto exc, const uint4 Ar, bool masked) __attribute__((always_inline)) {
+        auto blockA = [&](auto g0c, auto g1c, auto exc, const uint4 Ar, bool masked, const uint32_t (&xn)[4]) __attribute__((always_inline)) {
             constexpr int G0 = decltype(g0c)::value, G1 = decltype(g1c)::value;
             constexpr bool EX = decltype(exc)::value != 0;
             f4 D[NG + 1];
@@ -560,19 +594,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                     if (masked) {
                         const int i = 4 * (4 * kb + r) + rho; /* block 0 */
                         const uint32_t sv =
-                            (g == 0 || !EX) ? sad32(bits, mbv, 0u) : sad32(bits >> shg[g], kgv, 0u);
+                            (g == 0 || !EX) ? sad32(bits, mbv, 0u) : lpc_abs(bits, shg[g], kgv, xn[r], 0u);
                         acc[g] += i >= start_of(g) ? sv : 0u;
                     } else if (g == 0 || !EX) { /* opaque: one v_sad_u32 per value, not a reassociated min/max/sub */
                         acc[g] = opaque(sad32(bits, mbv, acc[g]));
                     } else {
-                        acc[g] = sad32(bits >> shg[g], kgv, acc[g]);
+                        acc[g] = lpc_abs(bits, shg[g], kgv, xn[r], acc[g]);
                     }
                 }
             }
         };
-        auto block = [&](auto g0c, auto g1c, auto exc, uint2 q, bool masked) __attribute__((always_inline)) {
-            blockA(g0c, g1c, exc, a_raw(q), masked);
+        auto block = [&](auto g0c, auto g1c, auto exc, uint2 q, bool masked, int blk) __attribute__((always_inline)) {
+            uint32_t xn[4];
+            ldx(blk, xn);
+            blockA(g0c, g1c, exc, a_raw(q), masked, xn);
         };
+        const uint32_t xnone[4] = {0u, 0u, 0u, 0u};
         /* per (group, order): sum over the 4 phases (quad, < 2^32) then, in 64 bits, over the
          * 4 kb rows; the lanes with rho == 0 and kb == 0 store.  BD: the LPC groups hold the
          * bound sum |T|, stored as floor(acc / 2^shift) per lane (a lower bound of the sum of
@@ -602,15 +639,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
             const bool no_lpc = a.stop_after == 12; /* ablation (timing only): no LPC bound at all */
             for (int k = wid == 0 ? 1 : 0; k < kw; ++k) {
                 const uint4 A = a_raw(ld(wid + k * nw));
-                blockA(I0{}, I0{}, I0{}, A, false);
-                if ((k & 3) == 0 && !no_lpc) blockA(I1{}, ING{}, I0{}, A, false);
+                blockA(I0{}, I0{}, I0{}, A, false, xnone);
+                if ((k & 3) == 0 && !no_lpc) blockA(I1{}, ING{}, I0{}, A, false, xnone);
             }
-            if (wid == 0) block(I0{}, ING{}, I0{}, ld0(), true);
+            if (wid == 0) block(I0{}, ING{}, I0{}, ld0(), true, 0);
             reduce_store(I0{}, I1{});
         } else {
-            for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I0{}, ING{}, I1{}, ld(blk), false);
-            if (wid == 0) block(I0{}, ING{}, I1{}, ld0(), true);
+            for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I0{}, ING{}, I1{}, ld(blk), false, blk);
+            if (wid == 0) block(I0{}, ING{}, I1{}, ld0(), true, 0);
             reduce_store(I0{}, I0{});
+            if constexpr (LIST) mv.tiers = 1 | (1 << 8); /* one exact pass (the listed units' marker) */
         }
         __syncthreads(); /* B2 */
         STAMP(3);
@@ -656,8 +694,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
                     __syncthreads(); /* every wave has read the bounds */
 #pragma unroll
                     for (int g = 1; g <= NG; ++g) acc[g] = 0;
-                    for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I1{}, ING{}, I1{}, ld(blk), false);
-                    if (wid == 0) block(I1{}, ING{}, I1{}, ld0(), true);
+                    for (int blk = wid == 0 ? nw : wid; blk < nblk; blk += nw) block(I1{}, ING{}, I1{}, ld(blk), false, blk);
+                    if (wid == 0) block(I1{}, ING{}, I1{}, ld0(), true, 0);
                     reduce_store(I1{}, I0{});
                     __syncthreads();
                     tj = lane_total();
@@ -1034,13 +1072,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
     if (lane < (1 << best)) rp[lane] = (int32_t)(pkw[(lane << (oo - best)) * RS + best] & 0x7fffu);
 }
 
-/* units the stream kernel listed (outside its MFMA bound) are handled by k_resid's list
- * variant, see launch_resid_bucket_list in k_resid.h */
+typedef const __attribute__((address_space(4))) ResidArgs* StreamKernarg;
+
+/* one workgroup per unit of the batch */
+template <int NG, bool R05, int NFIX = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7, 8))) void k_resid_stream(ResidArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    stream_unit<NG, R05, NFIX, false>(a, blockIdx.x, smem);
+}
+
+/* the units k_resid_stream listed (a.retry_list), pred-only taps: a fixed grid whose
+ * workgroups loop over the list (its length is known only on the device); an empty list costs
+ * one scalar load per workgroup */
+template <int NG, bool R05, int NFIX = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_resid_stream_list(ResidArgs a) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const unsigned long long cnt = *a.retry_count;
+    for (unsigned long long k = blockIdx.x; k < cnt; k += gridDim.x) {
+        /* the arguments through the kernarg pointer, opaque per unit: hoisted out of the loop,
+         * every field would stay live in registers across it */
+        StreamKernarg pa = (StreamKernarg)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(pa));
+        stream_unit<NG, R05, NFIX, true>(*pa, pa->retry_list[k], smem);
+        __syncthreads(); /* every wave is done with this unit's LDS */
+    }
+}
+
+/* units the list kernel could not take (sum|c| > 127) are handled by k_resid's list variant,
+ * see launch_resid_list in k_resid.h */
 hipError_t launch_resid_retry_l8(const ResidArgs& a, hipStream_t s);
 hipError_t launch_resid_retry_l12(const ResidArgs& a, hipStream_t s);
 
 bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes) {
-    if (!a.stream || path != 0 || residual_bytes != 4 || a.sample_bytes != 2 || !a.mfma || !a.retry_list || !a.retry_count)
+    if (!a.stream || path != 0 || residual_bytes != 4 || a.sample_bytes != 2 || !a.mfma || !a.retry_list || !a.retry_count ||
+        !a.retry2_list || !a.retry2_count)
         return false;
     const bool ref = a.mode == FLACMI_MODE_REFERENCE && a.L >= 1 && a.L <= 12;
     if (!ref && a.mode != FLACMI_MODE_FIXED_ONLY) return false;
@@ -1052,59 +1117,72 @@ bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes) {
     return true;
 }
 
-template <int NG, int NFIX>
-static hipError_t launch_stream_F(const ResidArgs& a, hipStream_t s) {
-    constexpr int nt = stream_threads(NFIX);
+/* the list kernel's grid: 16 workgroups per CU (the batch kernel's residency) */
+static unsigned stream_list_grid(int64_t count) {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+        ncu = 256;
+    const int64_t g = 16 * (int64_t)ncu;
+    return (unsigned)(count < g ? count : g);
+}
+
+template <int NG, bool R05, int NFIX>
+static hipError_t launch_stream_K(const ResidArgs& a, bool list, hipStream_t s) {
+    const int nt = NFIX ? stream_threads(NFIX) : stream_threads(a.n);
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
     const size_t lds = stream_lds(a.n, nt / 64, tap_table_words(NG), 1 << rmax_eff, kRiceOrders).total;
-    auto kern = k_resid_stream<NG, true, NFIX>;
+    auto kern = list ? k_resid_stream_list<NG, R05, NFIX> : k_resid_stream<NG, R05, NFIX>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)a.count), dim3(nt), lds, s, a);
+    hipLaunchKernelGGL(kern, dim3(list ? stream_list_grid(a.count) : (unsigned)a.count), dim3(nt), lds, s, a);
     return hipGetLastError();
 }
 
 template <int NG, bool R05>
-static hipError_t launch_stream_R(const ResidArgs& a, hipStream_t s) {
+static hipError_t launch_stream_R(const ResidArgs& a, bool list, hipStream_t s) {
     if constexpr (R05) /* the BASELINE configs' 4608-sample units at L = 4 NG: the constant-shape build */
-        if (a.n == 4608 && (NG == 0 || a.L == 4 * NG) && getenv("FLACMI_STREAM_GENERIC") == nullptr)
-            return launch_stream_F<NG, 4608>(a, s);
-    const int nt = stream_threads(a.n);
-    int rmax_eff = -1;
-    for (int o = a.rmin; o <= a.rmax; ++o)
-        if (a.n % (1 << o) == 0) rmax_eff = o;
-    const size_t lds = stream_lds(a.n, nt / 64, tap_table_words(NG), 1 << rmax_eff, kRiceOrders).total;
-    auto kern = k_resid_stream<NG, R05>;
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)a.count), dim3(nt), lds, s, a);
-    return hipGetLastError();
+        if (a.n == 4608 && (NG == 0 || a.L == 4 * NG) && knob(kKnobStreamGeneric) == 0)
+            return launch_stream_K<NG, true, 4608>(a, list, s);
+    return launch_stream_K<NG, R05, 0>(a, list, s);
 }
 
 template <int NG>
-static hipError_t launch_stream_T(const ResidArgs& a, hipStream_t s) {
+static hipError_t launch_stream_T(const ResidArgs& a, bool list, hipStream_t s) {
     /* partition orders 0..5 for every unit: rmin 0, rmax_eff 5 and n / 32 above the largest
      * predictor order (4 fixed, L for LPC) */
     int rmax_eff = -1;
     for (int o = a.rmin; o <= a.rmax; ++o)
         if (a.n % (1 << o) == 0) rmax_eff = o;
     const int maxord = NG > 0 && a.L > 4 ? a.L : 4;
-    if (a.rmin == 0 && rmax_eff == 5 && (a.n >> 5) > maxord) return launch_stream_R<NG, true>(a, s);
-    return launch_stream_R<NG, false>(a, s);
+    if (a.rmin == 0 && rmax_eff == 5 && (a.n >> 5) > maxord) return launch_stream_R<NG, true>(a, list, s);
+    return launch_stream_R<NG, false>(a, list, s);
 }
 
+static hipError_t launch_stream_G(const ResidArgs& a, bool list, hipStream_t s) {
+    if (a.mode == FLACMI_MODE_FIXED_ONLY) return launch_stream_T<0>(a, list, s);
+    if (a.L <= 4) return launch_stream_T<1>(a, list, s);
+    if (a.L <= 8) return launch_stream_T<2>(a, list, s);
+    return launch_stream_T<3>(a, list, s);
+}
+
+/* the batch, then (reference mode) the units it listed through the list kernel (pred-only
+ * taps), then the units that one listed through k_resid's list variant */
 hipError_t launch_resid_stream(const ResidArgs& a, hipStream_t s) {
     hipError_t e = hipMemsetAsync(a.retry_count, 0, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
-    if (a.mode == FLACMI_MODE_FIXED_ONLY) return launch_stream_T<0>(a, s); /* nothing is ever listed */
-    if (a.L <= 4) e = launch_stream_T<1>(a, s);
-    else if (a.L <= 8) e = launch_stream_T<2>(a, s);
-    else e = launch_stream_T<3>(a, s);
-    if (e != hipSuccess) return e;
+    if ((e = launch_stream_G(a, false, s)) != hipSuccess) return e;
+    if (a.mode == FLACMI_MODE_FIXED_ONLY) return hipSuccess; /* nothing is ever listed */
+    if ((e = hipMemsetAsync(a.retry2_count, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
     if ((e = launch_poison_lds(s)) != hipSuccess) return e;
-    return a.L <= 8 ? launch_resid_retry_l8(a, s) : launch_resid_retry_l12(a, s);
+    if ((e = launch_stream_G(a, true, s)) != hipSuccess) return e;
+    if ((e = launch_poison_lds(s)) != hipSuccess) return e;
+    ResidArgs b = a;
+    b.retry_count = a.retry2_count;
+    b.retry_list = a.retry2_list;
+    return a.L <= 8 ? launch_resid_retry_l8(b, s) : launch_resid_retry_l12(b, s);
 }
 
 }  // namespace flacmi

@@ -423,6 +423,14 @@ int64_t flacmi_unit_stride(int32_t block_len, int32_t sample_bytes);
 int flacmi_synth_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_t sample_bits,
                         int64_t unit_stride, int64_t first_unit, int64_t n_units, int32_t len,
                         uint64_t seed, void* stream);
+/* The same with open_eighths / 8 of the units (those whose hash byte is below open_eighths)
+ * replaced by MA(1) near-white noise, whose LPC candidates tie the fixed order-0 sum within a
+ * fraction of a percent: no bound decides them, so every candidate's exact sum is computed
+ * (bench.py --open, the "undecided" workload).  Bit-identical to oracle_synth_unit_mix;
+ * open_eighths = 0 is flacmi_synth_device. */
+int flacmi_synth_mix_device(flacmi_ctx* ctx, void* dst, int32_t sample_bytes, int32_t sample_bits,
+                            int64_t unit_stride, int64_t first_unit, int64_t n_units, int32_t len,
+                            uint64_t seed, int32_t open_eighths, void* stream);
 
 /* ---- device memory helpers (so hosts without a HIP binding can drive the device path) --- */
 void* flacmi_device_alloc(flacmi_ctx* ctx, size_t bytes);
@@ -438,6 +446,17 @@ int flacmi_synchronize(flacmi_ctx* ctx);
  * Synchronises on the recorded events; returns the number of values written. */
 int flacmi_last_timing(flacmi_ctx* ctx, float* ms, int n);
 int flacmi_timing_reset(flacmi_ctx* ctx);
+
+/* ---- test and diagnostic knobs ---------------------------------------------------------- */
+/* Process-wide knobs for A/B runs and tests, read from the environment once (the first time
+ * any is used) and changed afterwards only through flacmi_set_knob, so no launch calls getenv
+ * while another thread may change the environment.  Names: "FLACMI_OVERLAP" (analyze chunk
+ * overlap: -1 round-aligned (default), 0 off, k > 1 equal chunks, -R R units per round),
+ * "FLACMI_MF8_GRID" (cap on the int8-MFMA persistent grid, 0 = none), "FLACMI_STREAM_GENERIC"
+ * (1 = the runtime-shape stream kernel for 4608-sample units).  FLACMI_E_INVALID for any
+ * other name.  No device needed. */
+int flacmi_set_knob(const char* name, int32_t value);
+int flacmi_get_knob(const char* name, int32_t* value);
 
 /* ---- host-side views of the device arithmetic (for CPU verification of the helpers) ---- */
 /* Python float `x ** 2` as CPython 3.10 + glibc 2.35 pow (FMA variant) computes it;

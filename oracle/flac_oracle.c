@@ -484,6 +484,49 @@ static void sintab_init(void) {
         sintab[k] = (int32_t)nearbyint(32767.0 * libm_sin(6.283185307179586 * (double)k / 4096.0));
 }
 
+/* the width step shared by both recipes: a 16-bit value to `bits` bits (low random bits
+ * from the sample's hash when widening), clipped */
+static int32_t synth_widen(int64_t v, uint64_t r, int32_t bits) {
+    int64_t lo = -(1LL << (bits - 1)), hi = (1LL << (bits - 1)) - 1;
+    if (bits > 16) {
+        int e = bits - 16;
+        v = v * (1LL << e) + (int64_t)((r >> 32) & ((1ull << e) - 1)) - (1LL << (e - 1));
+    } else if (bits < 16) {
+        v >>= (16 - bits);
+    }
+    return (int32_t)(v < lo ? lo : (v > hi ? hi : v));
+}
+
+static int64_t synth_bsum(uint64_t r) {
+    return (int64_t)((r & 0xff) + ((r >> 8) & 0xff) + ((r >> 16) & 0xff) + ((r >> 24) & 0xff));
+}
+
+/* The "open" mix (bench.py --open K, DESIGN §4 "Undecided units"): a unit whose hash byte
+ * (h0 >> 56) & 7 is below open_eighths is MA(1) noise with a near-zero coefficient instead of
+ * tones: v_i = w_i + (a * w_{i-1} >> 7), w_i = (bsum_i - 510) * sg >> 7, a in -3..3 (rho <=
+ * 0.023), sg in 1024..4095.  Its LPC candidates tie the fixed order-0 sum within a fraction of a
+ * percent, so neither the sign bound nor the partial-sum tiers can decide it: every candidate's
+ * exact sum is computed (encoder.py:387-404, 537-548), and LPC wins about 4 units in 5.
+ * open_eighths = 0 is oracle_synth_unit. */
+void oracle_synth_unit_mix(int64_t unit, int32_t len, int32_t bits, uint64_t seed, int32_t open_eighths,
+                           int32_t* out) {
+    uint64_t h0 = splitmix64(seed ^ ((uint64_t)unit * 0xD1B54A32D192ED03ull));
+    if ((int32_t)((h0 >> 56) & 7) >= open_eighths) {
+        oracle_synth_unit(unit, len, bits, seed, out);
+        return;
+    }
+    int64_t sg = 1024 + (int64_t)(splitmix64(h0 + 5) % 3072);
+    int64_t a = (int64_t)(splitmix64(h0 + 6) % 7) - 3;
+    uint64_t base = seed ^ ((uint64_t)unit << 32);
+    int64_t wp = ((synth_bsum(splitmix64(base ^ (uint64_t)(int64_t)-1)) - 510) * sg) >> 7;
+    for (int i = 0; i < len; i++) {
+        uint64_t r = splitmix64(base ^ (uint64_t)i);
+        int64_t w = ((synth_bsum(r) - 510) * sg) >> 7;
+        out[i] = synth_widen(w + ((a * wp) >> 7), r, bits);
+        wp = w;
+    }
+}
+
 void oracle_synth_unit(int64_t unit, int32_t len, int32_t bits, uint64_t seed, int32_t* out) {
     pthread_once(&sintab_once, sintab_init);
     uint64_t h0 = splitmix64(seed ^ ((uint64_t)unit * 0xD1B54A32D192ED03ull));

@@ -45,6 +45,9 @@ int32_t oracle_floor_log2(double x, int32_t* status);                   /* floor
 
 /* Synthetic signal, bit-identical to flacmi_synth_device. */
 void oracle_synth_unit(int64_t unit, int32_t len, int32_t bits, uint64_t seed, int32_t* out);
+/* ... with open_eighths / 8 of the units MA(1) near-white noise (flacmi_synth_mix_device) */
+void oracle_synth_unit_mix(int64_t unit, int32_t len, int32_t bits, uint64_t seed, int32_t open_eighths,
+                           int32_t* out);
 
 #ifdef __cplusplus
 }

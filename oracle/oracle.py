@@ -65,6 +65,8 @@ def lib():
         L.oracle_floor_log2.restype = C.c_int32
         L.oracle_synth_unit.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_uint64, P(C.c_int32)]
         L.oracle_synth_unit.restype = None
+        L.oracle_synth_unit_mix.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_uint64, C.c_int32, P(C.c_int32)]
+        L.oracle_synth_unit_mix.restype = None
         _lib = L
     return _lib
 
@@ -199,16 +201,19 @@ def floor_log2(x: float):
     return r, st.value
 
 
-def synth_unit(unit: int, length: int, bits: int, seed: int) -> np.ndarray:
+def synth_unit(unit: int, length: int, bits: int, seed: int, open_eighths: int = 0) -> np.ndarray:
     out = np.zeros(length, dtype=np.int32)
-    lib().oracle_synth_unit(unit, length, bits, seed, _ptr(out, C.c_int32))
+    if open_eighths:
+        lib().oracle_synth_unit_mix(unit, length, bits, seed, open_eighths, _ptr(out, C.c_int32))
+    else:
+        lib().oracle_synth_unit(unit, length, bits, seed, _ptr(out, C.c_int32))
     return out
 
 
 def synth_batch(first_unit: int, n_units: int, length: int, bits: int, seed: int,
-                dtype=np.int16, stride: int = None) -> np.ndarray:
+                dtype=np.int16, stride: int = None, open_eighths: int = 0) -> np.ndarray:
     stride = stride or length
     a = np.zeros((n_units, stride), dtype=dtype)
     for i in range(n_units):
-        a[i, :length] = synth_unit(first_unit + i, length, bits, seed)
+        a[i, :length] = synth_unit(first_unit + i, length, bits, seed, open_eighths)
     return a

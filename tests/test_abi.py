@@ -73,6 +73,22 @@ def test_unit_stride_pads_4k_multiple_rows():
     assert lib.flacmi_unit_stride(0, 2) < 0 and lib.flacmi_unit_stride(16, 3) < 0
 
 
+def test_knobs_set_get_and_reject_unknown_names():
+    """flacmi_set_knob / flacmi_get_knob: the test knobs live in atomics, read from the
+    environment once; launches never call getenv."""
+    from flac_amd.analysis import get_knob, knob
+    lib = load()
+    for name in ("FLACMI_OVERLAP", "FLACMI_MF8_GRID", "FLACMI_STREAM_GENERIC"):
+        before = get_knob(name)
+        with knob(name, 7):
+            assert get_knob(name) == 7
+        assert get_knob(name) == before
+    assert lib.flacmi_set_knob(b"FLACMI_NOPE", 1) == abi.E_INVALID
+    assert b"unknown knob" in lib.flacmi_last_error()
+    v = ctypes.c_int32(0)
+    assert lib.flacmi_get_knob(None, ctypes.byref(v)) == abi.E_INVALID
+
+
 def test_create_without_device_fails_loudly():
     lib = load()
     if lib.flacmi_device_count() > 0:

@@ -32,3 +32,17 @@ def test_comm_world_one_allreduce_is_identity():
         assert torch.equal(v, want)
     finally:
         comm.close()
+
+
+def test_comm_two_devices_allreduce_sums_ranks(tmp_path):
+    """Two processes on devices 0 and 1 (skipped with fewer than two GPUs visible): rank 0's
+    flacmi_comm_id reaches rank 1 through a rendezvous directory, both build the communicator
+    with flacmi_comm_init and sum distinct stats vectors with flacmi_allreduce_stats; each rank
+    checks the sum of every rank's vector (tests/comm_child.py).  The CPU analogue with the same
+    hand-off and vectors over gloo is tests/test_multirank.py::test_comm_child_gloo_two_ranks."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("fewer than two GPUs visible")
+    import comm_child
+    comm_child.launch(2, "rccl", str(tmp_path), timeout=180)

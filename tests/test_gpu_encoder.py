@@ -157,6 +157,22 @@ def test_stream_c1_multi_context_matches_reference(enc, devices):
             (S["c1_correct"]["len"], S["c1_correct"]["sha256"])
 
 
+def test_stream_c1_two_devices_matches_reference(enc):
+    """encode(devices=[0, 1]): one context per GPU (skipped with fewer than two visible),
+    batches round-robin, frames merged in block order: byte-identical to the reference."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("fewer than two GPUs visible")
+    S = G.load("streams.json")
+    pcm = _sine(441000)
+    p = enc.EncoderParameters(block_size=4608, rice_partition_order=range(0, 6),
+                              lpc_order=range(0, 9), qlp_precision=5)
+    for bpb in (1, 5):
+        assert _stream(enc, 44100, 16, 1, len(pcm), [pcm], p, blocks_per_batch=bpb, devices=[0, 1]) == \
+            (S["c1_correct"]["len"], S["c1_correct"]["sha256"])
+
+
 def test_encode_planar_multi_context_and_frame_error_order(enc):
     """encode_planar over two contexts equals one context; a unit the reference fails on
     (an all-zero block: ZeroDivisionError in levinson_durbin) raises after exactly the

@@ -198,3 +198,11 @@ def test_open_stats_comm_falls_back_together():
     assert all(none for _, none, _ in res)
     assert "rank 1" in res[1][2] and "flacmi_comm_available" in res[1][2]
     assert res[0][2]  # rank 0 reports why too
+
+
+def test_comm_child_gloo_two_ranks(tmp_path):
+    """CPU analogue of tests/test_gpu_comm.py::test_comm_two_devices_allreduce_sums_ranks: the
+    same rank script, id hand-off through the rendezvous directory and per-rank vectors,
+    summed over gloo."""
+    import comm_child
+    comm_child.launch(2, "gloo", str(tmp_path), timeout=180)
