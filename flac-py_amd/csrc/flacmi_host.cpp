@@ -1272,7 +1272,8 @@ extern "C" int flacmi_encode_pipeline(flacmi_ctx* ctx, const flacmi_batch* batch
         };
         /* diagnostic (FLACMI_ENC_TRACE): per-sub-batch timeline in ms from the call's start */
         hipEvent_t tb = nullptr;
-        if (std::getenv("FLACMI_ENC_TRACE") && hipEventCreate(&tb) == hipSuccess) (void)hipEventRecord(tb, is);
+        static const bool trace = std::getenv("FLACMI_ENC_TRACE") != nullptr; /* read once */
+        if (trace && hipEventCreate(&tb) == hipSuccess) (void)hipEventRecord(tb, is);
         auto account = [&](int64_t k) {
             EncSlot& sl = slot[k % kEncSlots];
             (void)hipEventSynchronize(sl.e[7]);

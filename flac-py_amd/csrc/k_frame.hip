@@ -937,9 +937,14 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     FrameArgs b = a;
-    b.pack_split = (tiles == 1 || (nch + nt - 1) / nt <= kMaxC) && getenv("FLACMI_NO_PACK32") == nullptr;
-    const char* ab = getenv("FLACMI_PACK_ABLATE");
-    b.ablate = ab ? atoi(ab) : 0;
+    /* A/B and ablation switches, read once per process (no getenv per launch) */
+    static const bool no_pack32 = getenv("FLACMI_NO_PACK32") != nullptr;
+    static const int ablate = [] {
+        const char* e = getenv("FLACMI_PACK_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    b.pack_split = (tiles == 1 || (nch + nt - 1) / nt <= kMaxC) && !no_pack32;
+    b.ablate = ablate;
     if (b.pack_split) {
         hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
         if (e0 != hipSuccess) return e0;
