@@ -120,8 +120,10 @@ class Analyzer:
     # ------------------------------------------------------------------------------
     def analyze(self, samples: np.ndarray, params: abi.Params, block_len: int, tail_len: int = 0,
                 n_tail_units: int = 0, sample_bits: int = 16, residual_bytes: int = 4,
-                debug: bool = False) -> dict:
-        """Host arrays in, host arrays out (synchronous)."""
+                debug: bool = False, extras=()) -> dict:
+        """Host arrays in, host arrays out (synchronous).  debug: every optional output (acf,
+        fixed_sums, lpc_sums, lpc_records); extras: a subset of those names instead (lpc_sums
+        turns LPC pruning off, the others do not)."""
         s = np.ascontiguousarray(samples)
         if s.dtype not in (np.int16, np.int32) or s.ndim != 2:
             raise ValueError("samples must be a 2-D int16 or int32 array")
@@ -150,15 +152,13 @@ class Analyzer:
         o.residual = out["residual"].ctypes.data
         o.residual_bytes = residual_bytes
         o.residual_stride = rstride
-        if debug:
-            out["acf"] = np.zeros((n_units, 33), dtype=np.float64)
-            out["fixed_sums"] = np.zeros((n_units, 5), dtype=np.int64)
-            out["lpc_sums"] = np.zeros((n_units, 32), dtype=np.int64)
-            out["lpc_records"] = np.zeros((n_units, abi.lpc_rec_words(32)), dtype=np.int32)
-            o.acf = out["acf"].ctypes.data
-            o.fixed_sums = out["fixed_sums"].ctypes.data
-            o.lpc_sums = out["lpc_sums"].ctypes.data
-            o.lpc_records = out["lpc_records"].ctypes.data
+        want = ("acf", "fixed_sums", "lpc_sums", "lpc_records") if debug else tuple(extras)
+        shapes = {"acf": (33, np.float64), "fixed_sums": (5, np.int64), "lpc_sums": (32, np.int64),
+                  "lpc_records": (abi.lpc_rec_words(32), np.int32)}
+        for k in want:
+            w, dt = shapes[k]
+            out[k] = np.zeros((n_units, w), dtype=dt)
+            setattr(o, k, out[k].ctypes.data)
         check(self.lib.flacmi_analyze_host(self.ctx, C.byref(b), C.byref(params), C.byref(o)),
               "flacmi_analyze_host")
         wide = np.flatnonzero(out["meta"]["status"] == abi.STATUS_RESIDUAL_WIDE) if residual_bytes == 4 else []
@@ -167,7 +167,7 @@ class Analyzer:
             # rows and widen the batch's rows (the other units' results stand)
             first_tail = n_units - n_tail_units
             sub = self.analyze(np.ascontiguousarray(s[wide]), params, block_len, tail_len,
-                               int(np.count_nonzero(wide >= first_tail)), sample_bits, 8, debug)
+                               int(np.count_nonzero(wide >= first_tail)), sample_bits, 8, debug, extras)
             w = max(out["residual"].shape[1], sub["residual"].shape[1])
             res = np.zeros((n_units, w), dtype=np.uint64)
             res[:, :out["residual"].shape[1]] = out["residual"]

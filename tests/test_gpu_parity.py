@@ -909,6 +909,26 @@ def test_c3_int8_pruning_tiers_vs_oracle(az, n, q, L):
     assert want <= seen, want - seen
 
 
+def test_c3_fixed_sums_only_and_25bit_samples(az):
+    """k_resid_sb writes no fixed_sums rows, so a caller that asks for fixed_sums
+    alone (LPC pruning stays on) must take kVarMf8, which does; and k_resid_sb lists a unit
+    only when |x| > 2^23, so 25-bit input (x = +2^23 possible, its 32-bit K_j row sums assume
+    every term below 2^23) must not reach it.  Both against the oracle, every field."""
+    n, L, q = 16384, 32, 15
+    a = oracle.synth_batch(3100, 24, n, 24, 21, dtype=np.int32)
+    ora = oracle.analyze_batch(a, oracle.make_params(L, q, 0, 8), n, sample_bits=24, threads=16)
+    out = az.analyze(a, make_params(L, q, 0, 8), n, sample_bits=24, extras=("fixed_sums",))
+    compare_with_oracle(out, ora, [n] * len(a))
+    assert np.array_equal(out["fixed_sums"], ora["fixed_sums"])
+    assert (out["meta"]["lpc_order"] == abi.LPC_PRUNED).all()  # pruning stayed on
+    b = a.copy()
+    b[:, 5000] = 2 ** 23          # +2^23: 25 bits
+    b[::2, 9000] = -(2 ** 23)
+    orb = oracle.analyze_batch(b, oracle.make_params(L, 14, 0, 8), n, sample_bits=25, threads=16)
+    out = az.analyze(b, make_params(L, 14, 0, 8), n, sample_bits=25)
+    compare_with_oracle(out, orb, [n] * len(b))
+
+
 def test_mf8_persistent_grid_loops_over_units(az, monkeypatch):
     """kVarMf8's persistent grid (k_resid.h) with every workgroup looping over many units:
     FLACMI_MF8_GRID=4 caps it (and the 64-bit list variant's grid) at four workgroups, so the
