@@ -89,14 +89,13 @@ int main(int argc, char** argv) {
             all_terms += m;
             if (rhi <= rlo) { ++no_rect; continue; }
             rect_terms += rhi - rlo;
-            /* the taper chain up to the rectangle, tracking the record ulp exponent */
+            /* the taper chain up to the rectangle.  Its products are not integers, so after the
+             * accumulator drops to a lower binade the next add leaves bits at that binade's ulp:
+             * phi0 is a multiple of ulp(acc0), not of the coarsest ulp the taper reached */
             double acc = 0.0;
-            int grid = -1100; /* exponent of the coarsest ulp seen: phi is a multiple of 2^grid */
-            for (int j = 0; j < rlo; ++j) {
-                acc = acc + xw[j] * xw[j + l];
-                if (acc != 0.0) { int e = ilogb(acc) - 52; grid = e > grid ? e : grid; }
-            }
+            for (int j = 0; j < rlo; ++j) acc = acc + xw[j] * xw[j + l];
             const double acc0 = acc;
+            const int grid = acc0 != 0.0 ? ilogb(acc0) - 52 : -1100; /* phi0 is a multiple of 2^grid */
             /* truth: the sequential rectangle */
             for (int j = rlo; j < rhi; ++j) acc = acc + xw[j] * xw[j + l];
             const double truth = acc;
@@ -116,7 +115,12 @@ int main(int argc, char** argv) {
                 }
             }
             const double closed = (double)I + phi;
-            if (memcmp(&closed, &truth, sizeof(double)) != 0) ++theory_bad;
+            if (memcmp(&closed, &truth, sizeof(double)) != 0) {
+                ++theory_bad;
+                if (getenv("RECT_VERBOSE"))
+                    printf("  miss unit %d lag %d: acc0 %.17g grid 2^%d truth %.17g closed %.17g max|x|^2 2^%.1f\n", u, l, acc0,
+                           grid, truth, closed, log2((double)xm * (double)xm));
+            }
             const double phi0 = acc0 - floor(acc0);
             if (phi0 == 0.0) { ++phi_zero; continue; }
             /* provability from block sums */
