@@ -503,9 +503,11 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         if (int rc = ensure_buf(ctx->rec, sizeof(int32_t) * (size_t)rec_words * (size_t)(b->n_units > 0 ? b->n_units : 1)))
             return rc;
     }
-    /* fast-kernel retry lists: a counter, then one batch index per unit (k_resid_stream's list
-     * kernel hands units on through a second one behind it) */
-    if (int rc = ensure_buf(ctx->retry, sizeof(int64_t) * (size_t)(2 * b->n_units + 4))) return rc;
+    /* fast-kernel retry lists: 64 sub-list counters (k_resid_stream's batch kernel, 128 B apart),
+     * a counter and one batch index per unit (plus 64 for the sub-lists' rounding), then the
+     * second list through which k_resid_stream's list kernel hands units on */
+    constexpr int64_t kSubWords = 64 * 16;
+    if (int rc = ensure_buf(ctx->retry, sizeof(int64_t) * (size_t)(kSubWords + 2 * b->n_units + 68))) return rc;
     struct Cls {
         int64_t unit0, count;
         int n;
@@ -608,10 +610,12 @@ static int analyze_device_impl(flacmi_ctx* ctx, const flacmi_batch* b, const fla
         a.lpc_sums = o->lpc_sums ? o->lpc_sums + k.unit0 * 32 : nullptr;
         a.stop_after = debug_stop();
         a.mfma = use_mfma();
-        a.retry_count = (unsigned long long*)ctx->retry.p;
-        a.retry_list = (int64_t*)ctx->retry.p + 2;
-        a.retry2_count = (unsigned long long*)((int64_t*)ctx->retry.p + 2 + b->n_units);
-        a.retry2_list = (int64_t*)ctx->retry.p + 4 + b->n_units;
+        int64_t* const rb = (int64_t*)ctx->retry.p;
+        a.retry_sub = (unsigned long long*)rb;
+        a.retry_count = (unsigned long long*)(rb + kSubWords);
+        a.retry_list = rb + kSubWords + 2;
+        a.retry2_count = (unsigned long long*)(rb + kSubWords + 2 + b->n_units + 64);
+        a.retry2_list = rb + kSubWords + 4 + b->n_units + 64;
         a.sample_bits = b->sample_bits;
         a.stream = use_stream();
         a.prune = p->mode == FLACMI_MODE_REFERENCE && !o->lpc_sums && !(p->reserved[1] & FLACMI_FLAG_ALL_CANDIDATES) &&

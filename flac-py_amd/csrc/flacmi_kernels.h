@@ -56,6 +56,11 @@ struct ResidArgs {
     int64_t* retry_list;             /* and their batch indices (NULL: no fast path) */
     unsigned long long* retry2_count; /* k_resid_stream: the units its list kernel hands on to k_resid's */
     int64_t* retry2_list;             /* list variant (a second list of at most count entries) */
+    unsigned long long* retry_sub;    /* k_resid_stream's batch kernel lists unit u in sub-list u & 63: its
+                                         counter retry_sub[16 (u & 63)] (128 B apart), its entries
+                                         retry_list[(u & 63) retry_sub_cap ..] (one counter for every
+                                         workgroup serialised ~13 ns per listed unit at L2) */
+    int64_t retry_sub_cap;
     int32_t sample_bits;             /* declared sample width (bounds the 64-bit paths' narrow sums) */
     int32_t stream;                  /* 1 = k_resid_stream where the shape allows (env FLACMI_NO_STREAM=1 -> 0) */
     int32_t prune;                   /* 1 = reference mode may skip the exact LPC candidate sums of a unit

@@ -529,8 +529,14 @@ __device__ __forceinline__ void stream_unit(const Args& a, const int64_t gid, un
              * unit outside that bound too goes to k_resid's list variant */
             if (tid == 0) {
                 meta->status = FLACMI_STATUS_RETRY;
-                const unsigned long long k = atomicAdd(LIST ? a.retry2_count : a.retry_count, 1ull);
-                (LIST ? a.retry2_list : a.retry_list)[k] = gid;
+                if constexpr (LIST) {
+                    const unsigned long long k = atomicAdd(a.retry2_count, 1ull);
+                    a.retry2_list[k] = gid;
+                } else { /* sub-list gid & 63: 64 counters on their own cache lines */
+                    const int r = (int)(gid & 63);
+                    const unsigned long long k = atomicAdd(a.retry_sub + 16 * r, 1ull);
+                    a.retry_list[r * a.retry_sub_cap + (int64_t)k] = gid;
+                }
             }
             return;
         }
@@ -1087,13 +1093,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R05 ? 8 : 7
 template <int NG, bool R05, int NFIX = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_resid_stream_list(ResidArgs a) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const unsigned long long cnt = *a.retry_count;
-    for (unsigned long long k = blockIdx.x; k < cnt; k += gridDim.x) {
+    /* the batch kernel's 64 sub-lists: lane r holds the inclusive prefix of their lengths */
+    const int lane = threadIdx.x & 63;
+    uint32_t incl = (uint32_t)a.retry_sub[16 * lane];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, (unsigned)d);
+        if (lane >= d) incl += t;
+    }
+    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
         /* the arguments through the kernarg pointer, opaque per unit: hoisted out of the loop,
          * every field would stay live in registers across it */
         StreamKernarg pa = (StreamKernarg)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(pa));
-        stream_unit<NG, R05, NFIX, true>(*pa, pa->retry_list[k], smem);
+        const int r = __builtin_popcountll(__ballot(incl <= k)); /* incl[r - 1] <= k < incl[r] */
+        const uint32_t base = r > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)incl, r - 1) : 0u;
+        stream_unit<NG, R05, NFIX, true>(*pa, pa->retry_list[r * pa->retry_sub_cap + (k - base)], smem);
         __syncthreads(); /* every wave is done with this unit's LDS */
     }
 }
@@ -1105,7 +1121,7 @@ hipError_t launch_resid_retry_l12(const ResidArgs& a, hipStream_t s);
 
 bool stream_shape_ok(const ResidArgs& a, int path, int residual_bytes) {
     if (!a.stream || path != 0 || residual_bytes != 4 || a.sample_bytes != 2 || !a.mfma || !a.retry_list || !a.retry_count ||
-        !a.retry2_list || !a.retry2_count)
+        !a.retry2_list || !a.retry2_count || !a.retry_sub)
         return false;
     const bool ref = a.mode == FLACMI_MODE_REFERENCE && a.L >= 1 && a.L <= 12;
     if (!ref && a.mode != FLACMI_MODE_FIXED_ONLY) return false;
@@ -1170,8 +1186,10 @@ static hipError_t launch_stream_G(const ResidArgs& a, bool list, hipStream_t s) 
 
 /* the batch, then (reference mode) the units it listed through the list kernel (pred-only
  * taps), then the units that one listed through k_resid's list variant */
-hipError_t launch_resid_stream(const ResidArgs& a, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(a.retry_count, 0, sizeof(unsigned long long), s);
+hipError_t launch_resid_stream(const ResidArgs& a_in, hipStream_t s) {
+    ResidArgs a = a_in;
+    a.retry_sub_cap = (a.count + 63) / 64; /* sub-list u & 63 holds at most ceil(count / 64) units */
+    hipError_t e = hipMemsetAsync(a.retry_sub, 0, 64 * 16 * sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
     if ((e = launch_stream_G(a, false, s)) != hipSuccess) return e;
     if (a.mode == FLACMI_MODE_FIXED_ONLY) return hipSuccess; /* nothing is ever listed */
