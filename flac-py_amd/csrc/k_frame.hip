@@ -627,6 +627,16 @@ __global__ __launch_bounds__(kPackThreads) void k_pack(FrameArgs a) {
  * starts at 0), shifts it to E with the x^(8*2^b) tables and the workgroup XORs the
  * shares.  The frame is stored with 16-byte stores (dword / byte stores at its two ends).
  * ==================================================================================== */
+/* k_pack32: the w-bit field val (1 <= w <= 32) ORed into the window at bit P, one or two
+ * words (bit 31 of a window word is its first bit; the second OR is zero unless the field
+ * straddles a word boundary) */
+__device__ __forceinline__ void or_bits(uint32_t* win, uint32_t P, uint32_t val, uint32_t w) {
+    const uint64_t t = (uint64_t)val << (64u - (P & 31u) - w);
+    uint32_t* wp = win + (P >> 5);
+    atomicOr(wp, (uint32_t)(t >> 32));
+    atomicOr(wp + 1, (uint32_t)t);
+}
+
 template <int MAXC> /* chunks per thread the launch guarantees (2..kMaxC): fewer registers, more
                      * frames in flight per CU */
 __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
@@ -746,8 +756,11 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
             pa[j] = pb[j] = 0;
             bnd[j] = 1 << 30;
             if (k < k1) {
-                const uint4 v0 = *reinterpret_cast<const uint4*>(zrow + i0);
-                const uint4 v1 = *reinterpret_cast<const uint4*>(zrow + i0 + 4);
+                uint4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
+                if (!(a.ablate & 32)) { /* ablation 32: no residual loads (timing only) */
+                    v0 = *reinterpret_cast<const uint4*>(zrow + i0);
+                    v1 = *reinterpret_cast<const uint4*>(zrow + i0 + 4);
+                }
                 z[j][0] = v0.x; z[j][1] = v0.y; z[j][2] = v0.z; z[j][3] = v0.w;
                 z[j][4] = v1.x; z[j][5] = v1.y; z[j][6] = v1.z; z[j][7] = v1.w;
                 const int part0 = i0 / ps;
@@ -781,22 +794,11 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
         uint32_t pre_w = 0;
         for (int w2 = 0; w2 < wid; ++w2) pre_w += red[w2];
         uint32_t pos = s0 + pre + pre_w + v - tsum;
-        uint32_t widx = pos >> 5;
-        uint64_t acc = 0;
-        auto emit = [&](uint32_t wi, uint32_t val) __attribute__((always_inline)) {
-            if (val != 0) atomicOr(&win[wi], val);
-        };
-        /* val right-aligned, 1 <= w <= 32; keeps pos - 32*widx in [0, 32) */
-        auto put = [&](uint32_t val, int w) __attribute__((always_inline)) {
-            const int off = (int)(pos - 32u * widx);
-            acc |= (uint64_t)val << (64 - off - w);
-            pos += (uint32_t)w;
-            if (pos - 32u * widx >= 32u) {
-                emit(widx, (uint32_t)(acc >> 32));
-                acc <<= 32;
-                ++widx;
-            }
-        };
+        /* Every field lands in the zeroed window by LDS ORs at its bit position: a code's q unary
+         * zeros need no write, its terminating 1 and p low bits (<= 31 bits) take one or two ORs,
+         * and so does a partition's parameter.  No per-thread bit accumulator and no branch on
+         * where a word fills (round 6; the accumulator's emit branches and 64-bit shifts cost
+         * about 28 VALU per value). */
         const uint32_t pmask_m = (1u << method) - 1u;
 #pragma unroll
         for (int j = 0; j < MAXC; ++j) {
@@ -804,41 +806,44 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
             if (k < k1 && !(a.ablate & 2)) {
                 const int i0 = 8 * k;
                 const int part0 = pt0[j];
+                /* a chunk inside (order, n) whose values share one partition (the common case): at
+                 * most its first value opens a partition, so the parameter goes in before the
+                 * values, which then run straight-line */
+                if (i0 > order && i0 + 8 <= n && bnd[j] >= i0 + 8) {
+                    const int p = pa[j];
+                    if (i0 == part0 * ps) {
+                        or_bits(win, pos, (uint32_t)p & pmask_m, (uint32_t)method);
+                        pos += (uint32_t)method;
+                    }
+                    const uint32_t one = 1u << p, wc = (uint32_t)p + 1u;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int i = i0 + e;
-                    if (i >= order && i < n) {
-                        const int p = i >= bnd[j] ? pb[j] : pa[j];
-                        const bool first = i == order || (i > order && (i == bnd[j] || i == part0 * ps));
+                    for (int e = 0; e < 8; ++e) {
                         const uint32_t zk = z[j][e];
-                        const uint32_t qv = zk >> p;
-                        const uint32_t code = (1u << p) | (zk & ((1u << p) - 1u)); /* p <= 30: narrow values */
-                        /* usually the parameter, the q zeros and the code fit one put of <= 32 bits */
-                        uint32_t val = code, w = qv + 1u + (uint32_t)p;
-                        if (first) {
-                            if (w + (uint32_t)method <= 32u) {
-                                val |= ((uint32_t)p & pmask_m) << w;
-                                w += (uint32_t)method;
-                            } else {
-                                put((uint32_t)p & pmask_m, method);
+                        const uint32_t P = pos + (zk >> p);
+                        or_bits(win, P, one | (zk & (one - 1u)), wc);
+                        pos = P + wc;
+                    }
+                } else { /* the warm-up's chunk, the unit's end, a partition boundary inside */
+#pragma unroll 1
+                    for (int e = 0; e < 8; ++e) {
+                        uint32_t zk = z[j][0];
+#pragma unroll
+                        for (int e2 = 1; e2 < 8; ++e2) zk = e == e2 ? z[j][e2] : zk;
+                        const int i = i0 + e;
+                        if (i >= order && i < n) {
+                            const int p = i >= bnd[j] ? pb[j] : pa[j];
+                            if (i == order || i == bnd[j] || i == part0 * ps) {
+                                or_bits(win, pos, (uint32_t)p & pmask_m, (uint32_t)method);
+                                pos += (uint32_t)method;
                             }
-                        }
-                        if (w <= 32u) {
-                            put(val, (int)w);
-                        } else { /* long unary run */
-                            pos += qv;
-                            if (pos - 32u * widx >= 32u) {
-                                emit(widx, (uint32_t)(acc >> 32));
-                                acc = 0;
-                                widx = pos >> 5;
-                            }
-                            put(code, p + 1);
+                            const uint32_t P = pos + (zk >> p);
+                            or_bits(win, P, (1u << p) | (zk & ((1u << p) - 1u)), (uint32_t)p + 1u); /* p <= 30 */
+                            pos = P + (uint32_t)p + 1u;
                         }
                     }
                 }
             }
         }
-        if (pos != 32u * widx) emit(widx, (uint32_t)(acc >> 32));
         __syncthreads(); /* red[] reuse by the next subframe's scan */
     }
 
@@ -850,7 +855,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
         const int64_t b1 = E - seg * (NT - 1 - tid);
         const int64_t b0 = b1 - seg;
         uint32_t crc = 0;
-        if (b1 > F) {
+        if (b1 > F && !(a.ablate & 4)) { /* ablation 4: no CRC fold (timing only) */
             const int64_t r0 = b0 - Fa; /* may be negative: those bytes precede the frame */
             const int o = (int)(((E - Fa) & 3));
             for (int64_t r = r0; r < b1 - Fa; r += 4) {
@@ -891,7 +896,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
             if (B >= F && B < Fend && !(g >= gf && g < ge)) a.out[B] = (uint8_t)(win[g - g0] >> (24 - 8 * jj));
         }
     }
-    if (gf < ge) {
+    if (gf < ge && !(a.ablate & 16)) { /* ablation 16: no stores of the frame's body (timing only) */
         const int64_t mis = (int64_t)(((uintptr_t)a.out >> 2) & 3); /* out is 4-byte aligned */
         const int64_t ga = ((gf + mis + 3) & ~3LL) - mis; /* 16-byte aligned output words [ga, gz) */
         const int64_t gz = ((ge + mis) & ~3LL) - mis;
