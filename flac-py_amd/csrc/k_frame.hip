@@ -847,30 +847,32 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
         __syncthreads(); /* red[] reuse by the next subframe's scan */
     }
 
-    /* CRC-16 of bytes [F, E), E = Fend - 2.  Window byte r is frame byte F - (F & 3) + r. */
+    /* CRC-16 of bytes [F, E), E = Fend - 2.  Window byte r is frame byte F - (F & 3) + r; the
+     * bytes before F are zero, which a CRC that starts at 0 ignores.  Thread t folds whole window
+     * words [t spw, (t + 1) spw) of the nfull words before E (one aligned LDS read each, no byte
+     * funnel), the last thread also the 0..3 bytes after them, and each share is shifted to E by
+     * the x^(8 2^b) tables. */
     const int64_t E = Fend - 2;
     const int64_t Fa = F & ~3LL;
-    const int64_t seg = (((E - F) + NT - 1) / NT + 3) & ~3LL; /* bytes per thread, multiple of 4 */
     {
-        const int64_t b1 = E - seg * (NT - 1 - tid);
-        const int64_t b0 = b1 - seg;
+        const int nfull = (int)((E - Fa) >> 2);
+        const int spw = (nfull + NT - 1) / NT;
+        const int w0 = tid * spw, w1 = min(w0 + spw, nfull);
         uint32_t crc = 0;
-        if (b1 > F && !(a.ablate & 4)) { /* ablation 4: no CRC fold (timing only) */
-            const int64_t r0 = b0 - Fa; /* may be negative: those bytes precede the frame */
-            const int o = (int)(((E - Fa) & 3));
-            for (int64_t r = r0; r < b1 - Fa; r += 4) {
-                uint32_t w;
-                if (r + 4 <= 0) continue; /* wholly before the window */
-                const int64_t k = r >> 2; /* floor: r may be -1..-3 only when o != 0 */
-                const uint32_t lo = k >= 0 ? win[k] : 0u;
-                const uint32_t hi = (k + 1) < nwf ? win[k + 1] : 0u;
-                w = o ? ((lo << (8 * o)) | (hi >> (32 - 8 * o))) : lo;
-                /* bytes before F are zero in the window already (the frame's first word is
-                 * shared only in the output, not in this window) */
+        if (!(a.ablate & 4)) { /* ablation 4: no CRC fold (timing only) */
+            for (int k = w0; k < w1; ++k) {
+                const uint32_t w = win[k];
                 crc = (uint32_t)ct[3 * 256 + ((crc >> 8) ^ (w >> 24))] ^ (uint32_t)ct[2 * 256 + ((crc ^ (w >> 16)) & 0xFF)] ^
                       (uint32_t)ct[256 + ((w >> 8) & 0xFF)] ^ (uint32_t)ct[w & 0xFF];
             }
-            if (!(a.ablate & 1)) crc = crc16_mulpow(crc, E - b1, a.crc_pow);
+            int64_t d = E - (Fa + 4 * (int64_t)max(w1, w0)); /* bytes between the share's end and E */
+            if (tid == NT - 1) { /* the last bytes before E */
+                const uint32_t w = win[nfull];
+                for (int j = 0; j < (int)(E - Fa) - 4 * nfull; ++j)
+                    crc = ((crc << 8) & 0xFFFF) ^ (uint32_t)ct[(crc >> 8) ^ ((w >> (24 - 8 * j)) & 0xFF)];
+                d = 0;
+            }
+            if (!(a.ablate & 1)) crc = crc16_mulpow(crc, d, a.crc_pow);
         }
         for (int o2 = 32; o2 >= 1; o2 >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o2);
         if (lane == 0) red[wid] = crc;
