@@ -848,38 +848,51 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
     }
 
     /* CRC-16 of bytes [F, E), E = Fend - 2.  Window byte r is frame byte F - (F & 3) + r; the
-     * bytes before F are zero, which a CRC that starts at 0 ignores.  Thread t folds whole window
-     * words [t spw, (t + 1) spw) of the nfull words before E (one aligned LDS read each, no byte
-     * funnel), the last thread also the 0..3 bytes after them, and each share is shifted to E by
-     * the x^(8 2^b) tables. */
+     * bytes before F are zero, which a CRC that starts at 0 ignores.  The nfull whole window
+     * words before E are cut into NT equal segments of spw words (a power of two) that END at
+     * word nfull, so thread t's segment lies m = NT - 1 - t segments before it (the first ones
+     * reach below word 0: zeros).  Each thread folds its segment's words (one aligned LDS read
+     * each), then the shares combine in a tree: at level l the earlier block is shifted by the
+     * later block's 2^l segments, a multiplication by x^(8 * 4 spw 2^l), which is one level of
+     * the x^(8 2^b) tables, the same for every lane.  Thread 0 adds the waves, then shifts the
+     * whole by the 0..3 bytes between word nfull and E and folds those bytes. */
     const int64_t E = Fend - 2;
     const int64_t Fa = F & ~3LL;
     {
         const int nfull = (int)((E - Fa) >> 2);
-        const int spw = (nfull + NT - 1) / NT;
-        const int w0 = tid * spw, w1 = min(w0 + spw, nfull);
+        int ls = 0;
+        while ((NT << ls) < nfull) ++ls;
+        const int spw = 1 << ls;
+        const int w1 = nfull - (NT - 1 - tid) * spw, w0 = w1 - spw;
+        const uint16_t* __restrict__ pw = a.crc_pow;
+        auto mulx = [&](uint32_t c, int bl) __attribute__((always_inline)) { /* c * x^(8 * 2^bl) mod P */
+            return (uint32_t)pw[bl * 512 + (c & 0xFF)] ^ (uint32_t)pw[bl * 512 + 256 + (c >> 8)];
+        };
         uint32_t crc = 0;
         if (!(a.ablate & 4)) { /* ablation 4: no CRC fold (timing only) */
-            for (int k = w0; k < w1; ++k) {
+            for (int k = max(w0, 0); k < w1; ++k) {
                 const uint32_t w = win[k];
                 crc = (uint32_t)ct[3 * 256 + ((crc >> 8) ^ (w >> 24))] ^ (uint32_t)ct[2 * 256 + ((crc ^ (w >> 16)) & 0xFF)] ^
                       (uint32_t)ct[256 + ((w >> 8) & 0xFF)] ^ (uint32_t)ct[w & 0xFF];
             }
-            int64_t d = E - (Fa + 4 * (int64_t)max(w1, w0)); /* bytes between the share's end and E */
-            if (tid == NT - 1) { /* the last bytes before E */
-                const uint32_t w = win[nfull];
-                for (int j = 0; j < (int)(E - Fa) - 4 * nfull; ++j)
-                    crc = ((crc << 8) & 0xFFFF) ^ (uint32_t)ct[(crc >> 8) ^ ((w >> (24 - 8 * j)) & 0xFF)];
-                d = 0;
-            }
-            if (!(a.ablate & 1)) crc = crc16_mulpow(crc, d, a.crc_pow);
         }
-        for (int o2 = 32; o2 >= 1; o2 >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o2);
+        if (!(a.ablate & 1)) { /* ablation 1: no shift (timing only) */
+#pragma unroll
+            for (int l = 0; l < 6; ++l) {
+                const uint32_t other = (uint32_t)__shfl_xor((int)crc, 1 << l);
+                const bool right = (lane >> l) & 1;
+                crc = mulx(right ? other : crc, ls + 2 + l) ^ (right ? crc : other);
+            }
+        } else {
+            for (int o2 = 32; o2 >= 1; o2 >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, o2);
+        }
         if (lane == 0) red[wid] = crc;
         __syncthreads();
         if (tid == 0) {
             uint32_t x = 0;
-            for (int w2 = 0; w2 < NT / 64; ++w2) x ^= red[w2];
+            for (int w2 = 0; w2 < NT / 64; ++w2) x = (w2 ? mulx(x, ls + 8) : 0u) ^ red[w2]; /* 64 segments a wave */
+            const int tail = (int)(E - Fa) - 4 * nfull;
+            for (int j = 0; j < tail; ++j) x = ((x << 8) & 0xFFFF) ^ (uint32_t)ct[(x >> 8) ^ ((win[nfull] >> (24 - 8 * j)) & 0xFF)];
             win_or(win, 0, (uint32_t)(8 * (F & 3) + 8 * (E - F)), x & 0xFFFF, 16);
         }
         __syncthreads();
