@@ -769,13 +769,21 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
                 pa[j] = rp[part0];
                 pb[j] = (b1 < n && b1 <= i0 + 7) ? rp[part0 + 1] : pa[j];
                 bnd[j] = b1;
+                if (i0 > order && i0 + 8 <= n && b1 >= i0 + 8) { /* one partition, every value coded */
+                    const int p = pa[j];
+                    uint32_t q = 0;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const int i = i0 + e;
-                    const int p = i >= b1 ? pb[j] : pa[j];
-                    const bool valid = i >= order && i < n;
-                    const bool first = i == order || (i > order && (i == b1 || i == part0 * ps));
-                    tsum += valid ? (first ? (uint32_t)method : 0u) + (z[j][e] >> p) + 1u + (uint32_t)p : 0u;
+                    for (int e = 0; e < 8; ++e) q += z[j][e] >> p;
+                    tsum += q + 8u * (uint32_t)(p + 1) + (i0 == part0 * ps ? (uint32_t)method : 0u);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const int i = i0 + e;
+                        const int p = i >= b1 ? pb[j] : pa[j];
+                        const bool valid = i >= order && i < n;
+                        const bool first = i == order || (i > order && (i == b1 || i == part0 * ps));
+                        tsum += valid ? (first ? (uint32_t)method : 0u) + (z[j][e] >> p) + 1u + (uint32_t)p : 0u;
+                    }
                 }
             } else {
 #pragma unroll
