@@ -72,7 +72,7 @@ def get_knob(name: str) -> int:
 
 def set_knob(name: str, value: int) -> None:
     """Set a test/diagnostic knob (flacmi_set_knob): FLACMI_OVERLAP, FLACMI_MF8_GRID,
-    FLACMI_STREAM_GENERIC.  The library reads their environment variables once; this is the
+    FLACMI_STREAM_GENERIC, FLACMI_DECODE_GENERIC.  The library reads their environment variables once; this is the
     thread-safe way to change them afterwards."""
     check(load().flacmi_set_knob(name.encode(), int(value)), "flacmi_set_knob")
 

@@ -208,7 +208,7 @@ struct KnobDef {
     const char* name;
     int dflt;
 };
-constexpr KnobDef kKnobs[kKnobCount] = {{"FLACMI_OVERLAP", -1}, {"FLACMI_MF8_GRID", 0}, {"FLACMI_STREAM_GENERIC", 0}};
+constexpr KnobDef kKnobs[kKnobCount] = {{"FLACMI_OVERLAP", -1}, {"FLACMI_MF8_GRID", 0}, {"FLACMI_STREAM_GENERIC", 0}, {"FLACMI_DECODE_GENERIC", 0}};
 std::atomic<int> g_knob[kKnobCount];
 std::once_flag g_knob_once;
 void knobs_init() {
@@ -874,7 +874,9 @@ int flacmi_decode_frames_device(flacmi_ctx* ctx, const uint8_t* stream_data, int
         if (expect->n_tail_units && expect->tail_len > expect->block_len) return fail(FLACMI_E_INVALID, "expect: tail_len > block_len");
     }
     if (int rc = set_device(ctx)) return rc;
-    if (int rc = ensure_buf(ctx->dec, sizeof(int32_t) * (size_t)n_frames)) return rc;
+    /* workspace: decorr codes [n_frames] i32, the deferred-frame count (8 B) and list [n_frames] i64 */
+    const size_t dlist = (sizeof(int32_t) * (size_t)n_frames + 15) & ~(size_t)15;
+    if (int rc = ensure_buf(ctx->dec, dlist + 16 + sizeof(int64_t) * (size_t)n_frames)) return rc;
     DecodeArgs a{};
     a.words = reinterpret_cast<const uint32_t*>(stream_data);
     a.stream_bytes = stream_bytes;
@@ -900,6 +902,9 @@ int flacmi_decode_frames_device(flacmi_ctx* ctx, const uint8_t* stream_data, int
     a.status = frame_status;
     a.mismatch = frame_mismatch;
     a.decorr = (int32_t*)ctx->dec.p;
+    a.defer_count = (unsigned long long*)((char*)ctx->dec.p + dlist);
+    a.defer_list = (int64_t*)((char*)ctx->dec.p + dlist + 16);
+    a.defer_all = knob(kKnobDecodeGeneric) != 0;
     a.crc_slice = ctx->d_crc;
     HIP_TRY(launch_decode(a, (hipStream_t)stream));
     return 0;

@@ -122,6 +122,9 @@ struct DecodeArgs {
     int64_t* mismatch;       /* [n_frames] */
     int32_t* decorr;         /* [n_frames] scratch: (bs << 8) | channel code for k_decorr, else 0 */
     const uint16_t* crc_slice; /* [4][256] CRC-16 slice-by-4 tables */
+    unsigned long long* defer_count; /* frames k_decode_fx hands to k_decode: count, */
+    int64_t* defer_list;             /* and their indices ([n_frames]) */
+    int32_t defer_all;               /* knob FLACMI_DECODE_GENERIC: every frame through k_decode */
 };
 
 struct ResidLaunch {
@@ -135,7 +138,7 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes);
 constexpr int kMaxFinestParts = 4096;
 
 /* flacmi_set_knob's knobs: the environment's value (read once) or the last value set */
-enum Knob { kKnobOverlap = 0, kKnobMf8Grid, kKnobStreamGeneric, kKnobCount };
+enum Knob { kKnobOverlap = 0, kKnobMf8Grid, kKnobStreamGeneric, kKnobDecodeGeneric, kKnobCount };
 int knob(Knob k);
 
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);
@@ -163,7 +166,7 @@ hipError_t launch_stats(const flacmi_unit_meta* meta, int64_t n_units, int32_t b
 hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s);
 int64_t frame_scan_blocks(int64_t n_frames);
 hipError_t launch_pack(const FrameArgs& a, hipStream_t s);
-hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_decode(DecodeArgs a, hipStream_t s);
 
 hipError_t launch_selftest(int32_t which, const double* x, double* out, int32_t* status, int64_t n,
                            const double* log2thr, hipStream_t s);

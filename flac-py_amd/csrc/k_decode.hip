@@ -9,15 +9,28 @@
  * samples before it).  Frames, however, are independent and their byte offsets are known
  * (the writer's scan produced them), so:
  *
- *   k_decode   one LANE per frame.  Each lane walks its frame with a 64-bit big-endian
- *              bit window refilled one dword at a time (frames start at any byte) and
- *              decodes a Rice code with one v_ffbh.  Sample i of every lane's subframe is
- *              restored in loop iteration i, so the lanes of a wave stay in lock-step and
- *              the per-lane history ring in LDS (32 slots x 64 lanes, slot-major: a lane's
- *              column is one bank) is conflict-free.  Every 32 samples a lane flushes its
- *              ring column as 128 contiguous bytes of its decoded row and compares them with
- *              the source row.  CRC-8 / CRC-16 are recomputed from the frame bytes with the
- *              writer's slice-by-4 table (the reference reads them unchecked).
+ *   k_decode_fx  one LANE per frame, 256 frames per workgroup, for the frames every check
+ *              passes and whose subframes are CONSTANT, VERBATIM or FIXED (what the encoder
+ *              writes for almost every block: flac-py's negated LPC predictor rarely wins).
+ *              A FIXED sample is restored by four wrapping 32-bit adds (the order-k
+ *              predictor inverted as k running differences), a Rice code whose unary run
+ *              and low bits lie inside the 32-bit window by one v_ffbh, one shift-add and no
+ *              64-bit arithmetic; partition headers, escapes, long codes and the stream's
+ *              last dwords take a divergent general branch.  Decoded samples go through a
+ *              16-slot LDS ring per lane and are compared with the source rows every 16.
+ *              Any check that fails, an LPC subframe, wasted bits, stereo decorrelation or a
+ *              sample mismatch makes the lane hand its frame to the list below instead:
+ *              this kernel only ever reports status 0.
+ *   k_decode   one LANE per listed frame (or per frame, knob FLACMI_DECODE_GENERIC): the
+ *              general decoder with every check and the exact status precedence.  Sample
+ *              i of every lane's subframe is restored in loop iteration i, so the lanes of a
+ *              wave stay in lock-step and the per-lane history ring in LDS (32 slots x 64
+ *              lanes, slot-major: a lane's column is one bank) is conflict-free.  Every 32
+ *              samples a lane flushes its ring column as 128 contiguous bytes of its decoded
+ *              row and compares them with the source row.
+ *   Both read the frame with a 64-bit big-endian bit window refilled one dword at a time
+ *   (frames start at any byte) and fold the CRC-16 as whole dwords leave the window, with
+ *   the writer's slice-by-4 table (the reference reads CRC-8 / CRC-16 unchecked).
  *   k_decorr   frames whose header selects L_S / S_R / M_S stereo (flac-py's encoder never
  *              writes them) are recombined in place (decoder.py:431-448) and compared here,
  *              one workgroup per frame.
@@ -78,57 +91,66 @@ __device__ __forceinline__ int sample_size_of(int code) {
     }
 }
 
-/* MSB-first reader over the stream: `buf` holds the 64 bits that start at dword `bw`. */
+/* MSB-first reader over the stream: (hi, lo) are dwords b and b + 1 and the read position
+ * is 32 b + 32 - sh, sh in [0, 31], so the next 32 bits are one v_alignbit. */
 struct BitReader {
     const uint32_t* w;
     int64_t nw;
-    int64_t pos; /* absolute bit position */
-    int64_t bw;
-    uint64_t buf;
+    int64_t b;
+    uint32_t hi, lo;
+    int32_t sh;
+    int64_t bnear; /* b >= bnear: a 32-bit read could pass the stream's end */
+    bool near;
     /* CRC-16 of the frame folded as whole dwords leave the window, in stream order: dword
      * cnext is the next one due, dwords below cend are inside the CRC range (crc16_fused) */
     const uint16_t* ct = nullptr;
     uint32_t crc = 0;
     int64_t cnext = 0, cend = 0;
-    __device__ __forceinline__ uint32_t ld(int64_t i) const { return i < nw ? __builtin_bswap32(w[i]) : 0u; }
+    __device__ __forceinline__ uint32_t ld(int64_t i) const {
+        return (uint64_t)i < (uint64_t)nw ? __builtin_bswap32(w[i]) : 0u;
+    }
     __device__ __forceinline__ void fold(uint32_t be) { /* one whole big-endian dword */
         const uint32_t v = be ^ (crc << 16);
         crc = ct[3 * 256 + (v >> 24)] ^ ct[2 * 256 + ((v >> 16) & 0xFF)] ^ ct[256 + ((v >> 8) & 0xFF)] ^ ct[v & 0xFF];
     }
-    __device__ __forceinline__ void seek(int64_t p) {
-        pos = p;
-        bw = p >> 5;
-        buf = ((uint64_t)ld(bw) << 32) | ld(bw + 1);
+    __device__ __forceinline__ int64_t pos() const { return 32 * b + 32 - sh; }
+    __device__ __forceinline__ void seek(int64_t p, int64_t end_bit) {
+        b = (p - 1) >> 5; /* p = 0: dword -1 (reads as 0) */
+        sh = (int32_t)(32 * b + 32 - p);
+        hi = ld(b);
+        lo = ld(b + 1);
+        bnear = (end_bit >> 5) - 1;
+        near = b >= bnear;
     }
-    /* the 32 bits at pos, MSB first */
-    __device__ __forceinline__ uint32_t peek32() {
-        int64_t off = pos - (bw << 5);
-        if (off > 32) {
-            if (off < 64) {
-                if (ct && bw == cnext && bw < cend) { /* dword bw leaves the window */
-                    fold((uint32_t)(buf >> 32));
-                    ++cnext;
-                }
-                buf = (buf << 32) | ld(bw + 2);
-                bw += 1;
-                off -= 32;
-            } else {
-                seek(pos);
-                off = pos & 31;
-            }
+    __device__ __forceinline__ void adv() { /* dword b leaves the window */
+        if (ct && b == cnext && b < cend) {
+            fold(hi);
+            ++cnext;
         }
-        return (uint32_t)((buf << off) >> 32);
+        hi = lo;
+        lo = ld(b + 2);
+        ++b;
+        near = near || b >= bnear;
+    }
+    /* the 32 bits at the read position, MSB first */
+    __device__ __forceinline__ uint32_t peek32() const { return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)sh); }
+    __device__ __forceinline__ void skip(int n) { /* 0 <= n <= 32 */
+        sh -= n;
+        if (sh < 0) {
+            sh += 32;
+            adv();
+        }
     }
     __device__ __forceinline__ uint32_t uint(int n) { /* 0 <= n <= 32 (binary.py:97) */
         if (n == 0) return 0;
         const uint32_t v = peek32() >> (32 - n);
-        pos += n;
+        skip(n);
         return v;
     }
     __device__ __forceinline__ uint64_t uint64(int n) { /* 0 <= n <= 64 */
         if (n <= 32) return uint(n);
-        const uint64_t hi = uint(n - 32);
-        return (hi << 32) | uint(32);
+        const uint64_t hi2 = uint(n - 32);
+        return (hi2 << 32) | uint(32);
     }
     /* binary.py:129-131 (n >= 1) */
     __device__ __forceinline__ int64_t sint(int n) {
@@ -142,8 +164,8 @@ struct BitReader {
         uint32_t W = peek32();
         while (W == 0) {
             q += 32;
-            pos += 32;
-            if (pos > end) {
+            skip(32);
+            if (pos() > end) {
                 eof = true;
                 return 0;
             }
@@ -154,9 +176,9 @@ struct BitReader {
         uint64_t v;
         if (z + 1 + p <= 32) {
             v = (q << p) | (p ? ((W << (z + 1)) >> (32 - p)) : 0u);
-            pos += z + 1 + p;
+            skip(z + 1 + p);
         } else {
-            pos += z + 1;
+            skip(z + 1);
             v = (q << p) | uint(p);
         }
         return (int64_t)(v >> 1) ^ -(int64_t)(v & 1);
@@ -200,16 +222,9 @@ __device__ uint32_t crc16_range(const DecodeArgs& a, const uint16_t* t, int64_t 
     return c;
 }
 
-__global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
-    __shared__ int32_t ring[kRingSlots][kDecThreads];
-    __shared__ int16_t coef[kRingSlots][kDecThreads]; /* precision <= 15 bits (4-bit field, 15 rejected) */
-    __shared__ uint16_t crct[4 * 256];
-    const int lane = threadIdx.x;
-    for (int i = lane; i < 4 * 256; i += kDecThreads) crct[i] = a.crc_slice[i];
-    __syncthreads();
-
-    const int64_t f = (int64_t)blockIdx.x * kDecThreads + lane;
-    if (f >= a.n_frames) return;
+/* The general decoder: frame f, every check, the reference's exception precedence. */
+__device__ void decode_general(const DecodeArgs& a, const int64_t f, int32_t (*ring)[kDecThreads],
+                             int16_t (*coef)[kDecThreads], const uint16_t* crct, const int lane) {
     const int64_t F = a.offsets[f], Fend = a.offsets[f + 1];
     const int64_t end_bit = a.stream_bytes * 8; /* reading past it: EOFError */
     int64_t bad = 0;
@@ -231,9 +246,9 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
         g.cnext = Fh >> 2;
         g.cend = E >> 2;
     }
-    g.seek(F * 8);
+    g.seek(F * 8, end_bit);
     /* a parse failure after the reader ran off the stream is the EOFError of that read */
-    auto pfail = [&](int32_t site) { fail(g.pos > end_bit ? (int32_t)DS_EOF : site); };
+    auto pfail = [&](int32_t site) { fail(g.pos() > end_bit ? (int32_t)DS_EOF : site); };
 
     /* ---- frame header (decoder.py:133-245) ---- */
     int bs = 0, ss = 0, ch_code = 0, nch = 0;
@@ -262,9 +277,9 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
         else bs = 1 << bcode;
         if (rcode == 12) (void)g.uint(8);
         else if (rcode == 13 || rcode == 14) (void)g.uint(16);
-        const int hdr_bytes = (int)((g.pos >> 3) - F); /* byte-aligned here */
+        const int hdr_bytes = (int)((g.pos() >> 3) - F); /* byte-aligned here */
         const uint32_t crc8 = g.uint(8);
-        if (g.pos > end_bit) { pfail(DS_EOF); break; }
+        if (g.pos() > end_bit) { pfail(DS_EOF); break; }
         if (a.check_crc) {
             const uint8_t* bytes = reinterpret_cast<const uint8_t*>(a.words);
             uint32_t c = 0; /* x^8 + x^2 + x + 1, init 0 (crc.py:18-22) */
@@ -302,7 +317,7 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
         if (g.uint(1)) { /* get_wasted_bits: count zeros up to a one (parsed, not applied) */
             while (g.uint(1) == 0) {
                 ++wasted;
-                if (g.pos > end_bit) break;
+                if (g.pos() > end_bit) break;
             }
         }
         const int w = ss + (dbit ? 1 : 0) - wasted; /* sample_size_ (decoder.py:276) */
@@ -336,7 +351,7 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
                 shift = 0;
             }
         }
-        if (g.pos > end_bit) { fail(DS_EOF); break; }
+        if (g.pos() > end_bit) { fail(DS_EOF); break; }
         const int esc_code = (1 << pbits) - 1;
         /* FIXED subframes (the encoder's usual choice) predict from the last four samples held
          * in registers, not from the LDS ring; LPC subframes read the ring */
@@ -423,28 +438,28 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
                     }
                 }
             }
-            if (g.pos > end_bit) { fail(DS_EOF); break; }
+            if (g.pos() > end_bit) { fail(DS_EOF); break; }
         }
         if (is_ref_error(st)) break;
     }
     if (!is_ref_error(st) && nch > 0) {
         /* footer (decoder.py:124-128): zero padding to a byte, CRC-16 */
-        if (g.pos & 7) {
-            if (g.uint(8 - (int)(g.pos & 7)) != 0) pfail(DS_PADDING);
+        if (g.pos() & 7) {
+            if (g.uint(8 - (int)(g.pos() & 7)) != 0) pfail(DS_PADDING);
         }
         const uint32_t crc16 = g.uint(16);
-        if (g.pos > end_bit) fail(DS_EOF);
+        if (g.pos() > end_bit) fail(DS_EOF);
         else {
-            if ((g.pos >> 3) != Fend) fail(DS_FRAME_END);
+            if ((g.pos() >> 3) != Fend) fail(DS_FRAME_END);
             if (a.check_crc) {
                 uint32_t c;
-                if ((g.pos >> 3) == Fend && E > F) { /* the fused CRC: dwords not yet folded, then the tail */
+                if ((g.pos() >> 3) == Fend && E > F) { /* the fused CRC: dwords not yet folded, then the tail */
                     c = g.crc;
                     const int64_t d0 = g.cnext, d1 = g.cend;
                     if (d1 > d0) c = crc16_more(a, crct, c, 4 * d0, 4 * d1);
                     if (4 * d1 >= Fh) c = crc16_more(a, crct, c, 4 * d1 > Fh ? 4 * d1 : Fh, E);
                 } else {
-                    c = crc16_range(a, crct, F, (g.pos >> 3) - 2);
+                    c = crc16_range(a, crct, F, (g.pos() >> 3) - 2);
                 }
                 if (c != crc16) fail(DS_CRC16);
             }
@@ -455,6 +470,407 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
     a.status[f] = st;
     a.mismatch[f] = bad;
     a.decorr[f] = (decorr && !is_ref_error(st)) ? ((bs << 8) | ch_code) : 0;
+}
+
+/* The frames k_decode_fx listed (a.defer_all: every frame), one lane each. */
+__global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
+    __shared__ int32_t ring[kRingSlots][kDecThreads];
+    __shared__ int16_t coef[kRingSlots][kDecThreads]; /* precision <= 15 bits (4-bit field, 15 rejected) */
+    __shared__ uint16_t crct[4 * 256];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 4 * 256; i += kDecThreads) crct[i] = a.crc_slice[i];
+    __syncthreads();
+    const int64_t nl = a.defer_all ? a.n_frames : (int64_t)*a.defer_count;
+    for (int64_t k = (int64_t)blockIdx.x * kDecThreads + lane; k < nl; k += (int64_t)gridDim.x * kDecThreads)
+        decode_general(a, a.defer_all ? k : a.defer_list[k], ring, coef, crct, lane);
+}
+
+constexpr int kFxThreads = 256; /* k_decode_fx: frames per workgroup (one CRC table copy) */
+constexpr int kFxGroup = 8;     /* samples per comparison group (one 16- or 32-byte source load) */
+constexpr int kFxRing = 8;      /* stream dwords a lane keeps in LDS ahead of its bit window */
+
+/* k_decode_fx's reader.  Lanes read 64 unrelated frames, so a per-lane dword load that is
+ * waited for at once would stall the whole wave about every sample.  Instead the window's
+ * next dwords come from a per-lane LDS ring that the sample loop refills with one 16-byte
+ * load per lane every 4 samples, at points common to all lanes, and commits 4 samples later
+ * (the load has had those samples to land).  A lane that outruns its ring (long codes,
+ * headers) reads the stream directly.
+ * The window (hi, lo) is dwords k, k + 1 counted from the frame's first whole dword
+ * cw = ceil(F / 4) (k starts at -1 for every frame alignment); the read position is
+ * 32 (cw + k) + 32 - sh.  Ring slot j & 7 holds dword j for j in [k + 2, fe).  Dwords
+ * k in [0, nfold) are folded into the CRC-16 as they leave the window (decode_general's
+ * cnext / cend, relative). */
+struct FxReader {
+    const uint32_t* wb; /* dword cw */
+    int32_t nrel;       /* wb[0 .. nrel) lie inside the stream */
+    uint32_t hi, lo, crc;
+    int32_t sh, k, nfold, knear, fe; /* k >= knear: a 32-bit read could pass the stream's end */
+    uint32_t* sr;                    /* this lane's ring column: slot j at sr[j * kFxThreads] */
+    const uint16_t* ct;
+    __device__ __forceinline__ void fold(uint32_t be) {
+        const uint32_t v = be ^ (crc << 16);
+        crc = ct[3 * 256 + (v >> 24)] ^ ct[2 * 256 + ((v >> 16) & 0xFF)] ^ ct[256 + ((v >> 8) & 0xFF)] ^ ct[v & 0xFF];
+    }
+    __device__ __forceinline__ void adv() {
+        if ((uint32_t)k < (uint32_t)nfold) fold(hi);
+        hi = lo;
+        ++k;
+        const int32_t j = k + 1;
+        lo = j < fe ? sr[(j & (kFxRing - 1)) * kFxThreads] : ((uint32_t)j < (uint32_t)nrel ? __builtin_bswap32(wb[j]) : 0u);
+    }
+    /* bits read since the frame's first whole dword, minus 32 */
+    __device__ __forceinline__ int64_t rel() const { return 32 * (int64_t)k + 32 - sh; }
+    __device__ __forceinline__ uint32_t peek32() const { return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)sh); }
+    __device__ __forceinline__ void skip(int n) { /* 0 <= n <= 32 */
+        sh -= n;
+        if (sh < 0) {
+            sh += 32;
+            adv();
+        }
+    }
+    __device__ __forceinline__ uint32_t uint(int n) {
+        if (n == 0) return 0;
+        const uint32_t v = peek32() >> (32 - n);
+        skip(n);
+        return v;
+    }
+    __device__ __forceinline__ uint64_t uint64(int n) {
+        if (n <= 32) return uint(n);
+        const uint64_t h = uint(n - 32);
+        return (h << 32) | uint(32);
+    }
+    __device__ __forceinline__ int64_t sint(int n) {
+        const uint64_t x = uint64(n);
+        return n >= 64 ? (int64_t)x : (int64_t)(x << (64 - n)) >> (64 - n);
+    }
+    /* BitReader::rice with the end given relative (rel() > rend: past the stream's end) */
+    __device__ __forceinline__ int64_t rice(int p2, int64_t rend, bool& eof) {
+        uint64_t q = 0;
+        uint32_t W = peek32();
+        while (W == 0) {
+            q += 32;
+            skip(32);
+            if (rel() > rend) {
+                eof = true;
+                return 0;
+            }
+            W = peek32();
+        }
+        const int z = __builtin_clz(W);
+        q += z;
+        uint64_t v;
+        if (z + 1 + p2 <= 32) {
+            v = (q << p2) | (p2 ? ((W << (z + 1)) >> (32 - p2)) : 0u);
+            skip(z + 1 + p2);
+        } else {
+            skip(z + 1);
+            v = (q << p2) | uint(p2);
+        }
+        return (int64_t)(v >> 1) ^ -(int64_t)(v & 1);
+    }
+    /* the refill pipeline: the load issued at the previous refill point lands in the ring */
+    __device__ __forceinline__ void commit(const uint4& q) {
+        sr[((fe + 0) & (kFxRing - 1)) * kFxThreads] = __builtin_bswap32(q.x);
+        sr[((fe + 1) & (kFxRing - 1)) * kFxThreads] = __builtin_bswap32(q.y);
+        sr[((fe + 2) & (kFxRing - 1)) * kFxThreads] = __builtin_bswap32(q.z);
+        sr[((fe + 3) & (kFxRing - 1)) * kFxThreads] = __builtin_bswap32(q.w);
+        fe += 4;
+    }
+    /* dwords [fe, fe + 4) fit the ring and the stream: start their load */
+    __device__ __forceinline__ bool issue(uint4& q) {
+        fe = fe > k + 2 ? fe : k + 2;
+        if (fe + 4 - (k + 2) > kFxRing || fe + 4 > nrel) return false;
+        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4))); /* dwords: 4-byte aligned */
+        const u32x4a4 t = *reinterpret_cast<const u32x4a4*>(wb + fe);
+        q = uint4{t.x, t.y, t.z, t.w};
+        return true;
+    }
+};
+
+/* the subframe's last cnt < 8 samples (ring slots [0, cnt)), after its sample loop */
+template <int EB, bool OUT>
+__device__ __forceinline__ bool fx_part(int32_t (*ring)[kFxThreads], const int lane, const void* erow, int32_t* orow,
+                                        const int c0, const int cnt) {
+    uint32_t bad = 0;
+    for (int k = 0; k < cnt; ++k) {
+        const int32_t x = ring[k][lane];
+        if constexpr (OUT) orow[c0 + k] = x;
+        if constexpr (EB == 2) bad |= (uint32_t)(x ^ (int32_t)((const int16_t*)erow)[c0 + k]);
+        if constexpr (EB == 4) bad |= (uint32_t)(x ^ ((const int32_t*)erow)[c0 + k]);
+    }
+    return bad != 0;
+}
+
+/* k_decode_fx's frame: true when the frame decoded with every check passing and every sample
+ * equal to the source row (status 0, mismatch 0); false hands it to k_decode, which decodes
+ * it again from its first byte.  The checks are decode_general's, in its order, so a frame
+ * this function accepts is one decode_general gives status 0 (it never reports a failure
+ * itself). */
+template <int EB, bool OUT>
+__device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, int32_t (*ring)[kFxThreads],
+                                          int32_t (*wr)[kFxThreads], int32_t (*xr)[kFxThreads], uint32_t* sring,
+                                          const uint16_t* crct, const int lane) {
+    FxReader g;
+    int bs, nch, ss;
+    /* the stream's last bit, relative as rel() (derived from wb: not kept in registers) */
+    auto rend = [&]() __attribute__((always_inline)) { return a.stream_bytes * 8 - 32 * (int64_t)(g.wb - a.words); };
+    {
+        const int64_t F = a.offsets[f], Fend = a.offsets[f + 1];
+        const int64_t cw = (F + 3) >> 2, E = Fend - 2;
+        const int32_t fo = (int32_t)(32 * cw - 8 * F); /* frame-relative bit position = rel() + fo */
+        g.wb = a.words + cw;
+        const int64_t nr = a.n_words - cw;
+        g.nrel = nr < 0 ? 0 : nr > 0x7fffffff ? 0x7fffffff : (int32_t)nr;
+        g.hi = (cw - 1 >= 0 && cw - 1 < a.n_words) ? __builtin_bswap32(a.words[cw - 1]) : 0u;
+        g.lo = cw < a.n_words ? __builtin_bswap32(a.words[cw]) : 0u;
+        g.sh = fo;
+        g.k = -1;
+        g.fe = 1;
+        g.sr = sring + lane;
+        const int64_t kn = ((a.stream_bytes * 8) >> 5) - 1 - cw;
+        g.knear = kn < -1 ? -1 : kn > 0x7fffffff ? 0x7fffffff : (int32_t)kn;
+        g.ct = crct;
+        g.crc = 0;
+        g.nfold = 0;
+        if (a.check_crc && E > F) {
+            const int64_t nf = (E >> 2) - cw;
+            g.nfold = nf < 0 ? 0 : nf > 0x7fffffff ? 0x7fffffff : (int32_t)nf;
+            g.crc = crc16_more(a, crct, 0u, F, E < 4 * cw ? E : 4 * cw);
+        }
+
+        /* ---- frame header (decoder.py:133-245) ---- */
+        if (g.uint(15) != 0x7FFC) return false;
+        (void)g.uint(1);
+        const int bcode = g.uint(4);
+        if (!(bcode > 0 && bcode < 15)) return false;
+        const int rcode = g.uint(4);
+        if (rcode == 15) return false;
+        const int ch_code = g.uint(4);
+        if (ch_code > 7) return false; /* stereo decorrelation (8..10) and reserved codes: k_decode */
+        const int scode = g.uint(3);
+        if (scode == 3) return false;
+        if (g.uint(1) != 0) return false;
+        const uint32_t b0 = g.uint(8);
+        const int extra = b0 >= 0xFE ? 6 : b0 >= 0xFC ? 5 : b0 >= 0xF8 ? 4 : b0 >= 0xF0 ? 3 : b0 >= 0xE0 ? 2 : b0 >= 0xC0 ? 1 : 0;
+        uint64_t fno = extra == 0 ? b0 : (b0 & ((1u << (6 - extra)) - 1));
+        for (int k = 0; k < extra; ++k) fno = (fno << 6) | (g.uint(8) & 0x3F);
+        if (bcode == 1) bs = 192;
+        else if (bcode <= 5) bs = 144 << bcode;
+        else if (bcode == 6) bs = (int)g.uint(8) + 1;
+        else if (bcode == 7) bs = (int)g.uint(16) + 1;
+        else bs = 1 << bcode;
+        if (rcode == 12) (void)g.uint(8);
+        else if (rcode == 13 || rcode == 14) (void)g.uint(16);
+        const int hdr_bytes = (int)((g.rel() + fo) >> 3);
+        const uint32_t crc8 = g.uint(8);
+        if (g.rel() > rend()) return false;
+        if (a.check_crc) {
+            const uint8_t* bytes = reinterpret_cast<const uint8_t*>(a.words);
+            uint32_t c = 0;
+            for (int k = 0; k < hdr_bytes; ++k) {
+                c ^= bytes[F + k];
+                for (int bt = 0; bt < 8; ++bt) c = (c & 0x80) ? ((c << 1) ^ 0x07) & 0xFF : (c << 1) & 0xFF;
+            }
+            if (c != crc8) return false;
+        }
+        ss = scode == 0 ? a.sample_size : sample_size_of(scode);
+        nch = ch_code == 1 ? a.channels : ch_code + 1;
+        if (nch != a.channels) return false;
+        if (a.first_frame >= 0 && (int64_t)fno != a.first_frame + f) return false;
+        if (OUT && bs > a.out_stride) return false;
+    }
+
+    /* ---- subframes: CONSTANT, VERBATIM, FIXED (decoder.py:267-421, 473-498) ---- */
+    for (int c = 0; c < nch; ++c) {
+        const int64_t u = f * a.channels + c;
+        if (EB && unit_len_d(a, u) != bs) return false;
+        const void* erow = EB == 2 ? (const void*)((const int16_t*)a.expect + u * a.expect_stride)
+                                   : (const void*)((const int32_t*)a.expect + u * a.expect_stride);
+        int32_t* orow = OUT ? a.out + u * a.out_stride : nullptr;
+        if (g.uint(1) != 0) return false;
+        const int t = g.uint(6);
+        if (!(t <= 1 || (t >= 8 && t <= 12))) return false; /* LPC (and invalid types): k_decode */
+        if (g.uint(1)) return false;                        /* wasted bits: k_decode */
+        const int w = ss;
+        if (t <= 1) {
+            const int64_t cval = t == 0 ? g.sint(w) : 0;
+            for (int i = 0; i < bs; ++i) {
+                ring[i & (kFxGroup - 1)][lane] = (int32_t)(t == 0 ? cval : g.sint(w));
+                if ((i & (kFxGroup - 1)) == kFxGroup - 1 || i == bs - 1)
+                    if (fx_part<EB, OUT>(ring, lane, erow, orow, i & ~(kFxGroup - 1), (i & (kFxGroup - 1)) + 1)) return false;
+                if (g.rel() > rend()) return false;
+            }
+            continue;
+        }
+        /* FIXED: the warm-up samples, then x[i] = r + the order-k prediction, restored as k
+         * running differences: with d_j = Delta^j x[i-1], Delta^k x[i] = r and Delta^j x[i] =
+         * Delta^(j+1) x[i] + d_j.  Wrapping 32-bit arithmetic gives the reference's value
+         * modulo 2^32, which is what the int32 ring keeps (decode_general: int32 history). */
+        const int order = t & 7;
+        uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+        for (int k = 0; k < order; ++k) {
+            const uint32_t x = (uint32_t)g.sint(w);
+            wr[k][lane] = (int32_t)x;
+            const uint32_t u1 = x - d0, u2 = u1 - d1, u3 = u2 - d2;
+            d0 = x;
+            d1 = u1;
+            d2 = u2;
+            d3 = u3;
+        }
+        /* the levels the order uses, as lane masks (v_cndmask on SGPR pairs, no VGPRs) */
+        const bool m0 = order > 0, m1 = order > 1, m2 = order > 2, m3 = order > 3;
+        d0 = m0 ? d0 : 0u;
+        d1 = m1 ? d1 : 0u;
+        d2 = m2 ? d2 : 0u;
+        d3 = m3 ? d3 : 0u;
+        const int cm = g.uint(2);
+        if (cm > 1) return false;
+        const int pbits = cm ? 5 : 4;
+        const int po = g.uint(4);
+        if ((bs & ((1 << po) - 1)) != 0 || (bs >> po) <= order) return false;
+        const int plen = bs >> po;
+        if (g.rel() > rend()) return false;
+        int rem = 0, next = plen - order, param = 0;
+        bool esc = false;
+        /* the sample loop runs in blocks of 4 samples common to the lanes of the wave; at
+         * each block the stream refill (commit the previous 16-byte load, start the next)
+         * and the source-row pipeline (commit this block's 4 samples, loaded one block
+         * earlier, into the lane's LDS slots; start the next block's load) */
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        typedef typename std::conditional<EB == 4, u32x4, u32x2>::type ExpV;
+        auto exp_load = [&](int i) __attribute__((always_inline)) -> ExpV {
+            return EB == 4 ? *reinterpret_cast<const ExpV*>((const int32_t*)erow + i)
+                           : *reinterpret_cast<const ExpV*>((const int16_t*)erow + i);
+        };
+        ExpV qe{};
+        bool einflight = false;
+        if (EB && bs >= 4) {
+            qe = exp_load(0);
+            einflight = true;
+        }
+        uint4 q;
+        bool inflight = false;
+        uint32_t bad = 0;
+        bool fail = false;
+        for (int i0 = 0; i0 < bs; i0 += 4) {
+            if (inflight) g.commit(q);
+            if (EB && einflight) {
+                int32_t e[4];
+                if constexpr (EB == 4) {
+                    e[0] = (int32_t)qe[0], e[1] = (int32_t)qe[1], e[2] = (int32_t)qe[2], e[3] = (int32_t)qe[3];
+                } else {
+                    e[0] = (int32_t)(qe[0] << 16) >> 16, e[1] = (int32_t)qe[0] >> 16;
+                    e[2] = (int32_t)(qe[1] << 16) >> 16, e[3] = (int32_t)qe[1] >> 16;
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) xr[kk][lane] = e[kk];
+            }
+            inflight = g.issue(q);
+            einflight = EB && i0 + 8 <= bs;
+            if (einflight) qe = exp_load(i0 + 4);
+#pragma unroll 1
+            for (int kk = 0; kk < 4; ++kk) {
+                const int i = i0 + kk;
+                if (i < bs) {
+                    uint32_t x;
+                    if (i < order) {
+                        x = (uint32_t)wr[i][lane];
+                    } else {
+                        const uint32_t W = g.peek32();
+                        const int z = __builtin_clz(W | 1u);
+                        const int nb = z + 1 + param;
+                        uint32_t r;
+                        if (W == 0 || nb > 32 || rem == 0 || esc || g.k >= g.knear) {
+                            if (rem == 0) { /* get_rice_partition (decoder.py:400-411) */
+                                rem = next;
+                                next = plen;
+                                param = g.uint(pbits);
+                                esc = param == (1 << pbits) - 1;
+                                if (esc) {
+                                    param = g.uint(5); /* the escaped partition's sample width */
+                                    if (param == 0) fail = true;
+                                }
+                            }
+                            bool eof = false;
+                            r = (uint32_t)(esc ? g.sint(param) : g.rice(param, rend(), eof));
+                            if (eof || g.rel() > rend()) fail = true;
+                        } else {
+                            /* the unary run (z zeros), the stop bit and param low bits lie in
+                             * W: (W << z) >> (31 - param) = 2^param + low, so v = (z << param)
+                             * + low; no read can pass the stream's end (k < knear) */
+                            const uint32_t v = ((W << z) >> (31 - param)) + ((uint32_t)(z - 1) << param);
+                            g.skip(nb);
+                            r = (v >> 1) ^ (0u - (v & 1u));
+                        }
+                        --rem;
+                        const uint32_t u3 = r + d3, u2 = u3 + d2, u1 = u2 + d1;
+                        x = u1 + d0;
+                        d0 = m0 ? x : 0u;
+                        d1 = m1 ? u1 : 0u;
+                        d2 = m2 ? u2 : 0u;
+                        d3 = m3 ? u3 : 0u;
+                    }
+                    if constexpr (OUT) orow[i] = (int32_t)x;
+                    if constexpr (EB != 0) {
+                        /* a block that ends past bs has no committed slots: the row directly */
+                        const int32_t e = i0 + 4 <= bs ? xr[kk][lane]
+                                                      : (EB == 2 ? (int32_t)((const int16_t*)erow)[i] : ((const int32_t*)erow)[i]);
+                        bad |= x ^ (uint32_t)e;
+                    }
+                }
+            }
+            if (fail || bad) break; /* a failed check (escape width 0, end of stream) or a difference */
+        }
+        if (inflight) g.commit(q);
+        if (fail || bad) return false;
+    }
+    /* ---- footer (decoder.py:124-128) ---- */
+    if (g.rel() & 7) {
+        if (g.uint(8 - (int)(g.rel() & 7)) != 0) return false;
+    }
+    const uint32_t crc16 = g.uint(16);
+    if (g.rel() > rend()) return false;
+    /* re-read (volatile: not kept live in registers through the sample loops) */
+    const int64_t F = *(volatile const int64_t*)(a.offsets + f), Fend = *(volatile const int64_t*)(a.offsets + f + 1);
+    const int64_t cw = (F + 3) >> 2, E = Fend - 2;
+    if (((g.rel() + 32 * cw - 8 * F) >> 3) != Fend - F) return false;
+    if (a.check_crc) {
+        uint32_t c = g.crc;
+        if (E > F) {
+            /* dwords [cw + min(max(k, 0), nfold), cw + nfold) have not left the window yet */
+            const int32_t done = g.k < 0 ? 0 : g.k < g.nfold ? g.k : g.nfold;
+            if (g.nfold > done) c = crc16_more(a, crct, c, 4 * (cw + done), 4 * (cw + g.nfold));
+            if ((E >> 2) >= cw) c = crc16_more(a, crct, c, 4 * (E >> 2) > 4 * cw ? 4 * (E >> 2) : 4 * cw, E);
+        } else {
+            c = crc16_range(a, crct, F, E);
+        }
+        if (c != crc16) return false;
+    }
+    return true;
+}
+
+template <int EB, bool OUT>
+__global__ __launch_bounds__(kFxThreads) __attribute__((amdgpu_waves_per_eu(EB == 0 && !OUT ? 8 : 7, 8))) void k_decode_fx(DecodeArgs a) {
+    /* per-lane columns: a CONSTANT / VERBATIM subframe's samples between flushes (8 slots), or
+     * a FIXED subframe's warm-up samples (slots 0..3) and the source row's current block of 4
+     * (slots 4..7); a lane is in one kind of subframe at a time */
+    __shared__ int32_t ring[kFxGroup][kFxThreads];
+    __shared__ uint32_t sring[kFxRing * kFxThreads];
+    __shared__ uint16_t crct[4 * 256];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 4 * 256; i += kFxThreads) crct[i] = a.crc_slice[i];
+    __syncthreads();
+    const int64_t f = (int64_t)blockIdx.x * kFxThreads + lane;
+    if (f >= a.n_frames) return;
+    if (decode_fx<EB, OUT>(a, f, ring, ring, ring + 4, sring, crct, lane)) {
+        a.status[f] = 0;
+        a.mismatch[f] = 0;
+        a.decorr[f] = 0;
+    } else {
+        const unsigned long long k = atomicAdd(a.defer_count, 1ull);
+        a.defer_list[k] = f;
+    }
 }
 
 /* Interchannel decorrelation (decoder.py:431-448) of the frames k_decode marked, in place,
@@ -489,9 +905,28 @@ __global__ __launch_bounds__(256) void k_decorr(DecodeArgs a) {
     }
 }
 
-hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
+hipError_t launch_decode(DecodeArgs a, hipStream_t s) {
     if (a.n_frames <= 0) return hipSuccess;
-    const int64_t blocks = (a.n_frames + kDecThreads - 1) / kDecThreads;
+    int64_t blocks = (a.n_frames + kDecThreads - 1) / kDecThreads;
+    if (!a.defer_all && !(a.expect && !a.expect_vec) && !(a.out && (a.out_stride & 3))) {
+        hipError_t e = hipMemsetAsync(a.defer_count, 0, sizeof(unsigned long long), s);
+        if (e != hipSuccess) return e;
+        const dim3 g((unsigned)((a.n_frames + kFxThreads - 1) / kFxThreads)), b(kFxThreads);
+        const int eb = a.expect ? a.expect_bytes : 0;
+        if (a.out) {
+            if (eb == 2) hipLaunchKernelGGL((k_decode_fx<2, true>), g, b, 0, s, a);
+            else if (eb == 4) hipLaunchKernelGGL((k_decode_fx<4, true>), g, b, 0, s, a);
+            else hipLaunchKernelGGL((k_decode_fx<0, true>), g, b, 0, s, a);
+        } else {
+            if (eb == 2) hipLaunchKernelGGL((k_decode_fx<2, false>), g, b, 0, s, a);
+            else if (eb == 4) hipLaunchKernelGGL((k_decode_fx<4, false>), g, b, 0, s, a);
+            else hipLaunchKernelGGL((k_decode_fx<0, false>), g, b, 0, s, a);
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        blocks = blocks < 2048 ? blocks : 2048; /* the listed frames: a grid-stride loop */
+    } else {
+        a.defer_all = 1; /* rows k_decode_fx cannot read with 16-byte accesses: every frame general */
+    }
     hipLaunchKernelGGL(k_decode, dim3((unsigned)blocks), dim3(kDecThreads), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !a.out) return e;

@@ -6,6 +6,8 @@
 2. Round trip (BASELINE config 5 and the other config shapes): frames written by the
    device encoder decode on the device to exactly the source units, with CRC-8/16, frame
    numbers, frame ends and block sizes verified, and a corrupted byte is caught.
+Every test runs twice: with k_decode_fx taking the frames it accepts (the default) and with
+the FLACMI_DECODE_GENERIC knob sending every frame through the general k_decode.
 """
 import hashlib
 import json
@@ -16,16 +18,18 @@ import pytest
 
 import oracle
 from flac_amd import abi
+from flac_amd.analysis import knob
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "decode.json")
 
 
-@pytest.fixture(scope="module")
-def az():
+@pytest.fixture(scope="module", params=["fx", "generic"])
+def az(request):
     from flac_amd.analysis import Analyzer
     a = Analyzer(0)
-    yield a
+    with knob("FLACMI_DECODE_GENERIC", int(request.param == "generic")):
+        yield a
     a.close()
 
 
@@ -136,3 +140,31 @@ def test_crc16_fused_in_the_bit_reader(az):
     assert sorted(i for i, s in enumerate(st) if s) == sorted(picks)
     assert all((int(st[f]) >> 16) == abi.DSITE["crc16"] for f in picks)
     assert not mm.any()
+
+
+def test_fast_and_general_decoders_agree_on_damaged_streams(az):
+    """k_decode_fx hands every frame it cannot vouch for to k_decode: on a stream with LPC
+    frames and bytes damaged at many places, the default split and the all-general run give
+    the same status and mismatch count for every frame, and the same samples where status is 0."""
+    rng = np.random.default_rng(5)
+    for name in ("lpc_heavy_q15", "c2", "wide20"):
+        rows, data, offsets, (C, n, tail, n_tail, ss, first) = _encode(az, name)
+        bad = data.copy()
+        nf = len(offsets) - 1
+        hit = rng.choice(nf, size=max(3, nf // 4), replace=False)
+        for f in hit:
+            o0, o1 = int(offsets[f]), int(offsets[f + 1])
+            pos = int(rng.integers(o0, o1))
+            bad[pos] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        res = {}
+        for gen in (0, 1):
+            with knob("FLACMI_DECODE_GENERIC", gen):
+                res[gen] = az.decode_frames(bad, offsets, C, ss, first_frame=first, expect=rows, block_len=n,
+                                            tail_len=tail, n_tail_units=n_tail)
+        (o0, s0, m0), (o1, s1, m1) = res[0], res[1]
+        assert np.array_equal(s0, s1), name
+        assert np.array_equal(m0, m1), name
+        assert s0.any(), name
+        for f in range(nf):
+            if s0[f] == 0:
+                assert np.array_equal(o0[f * C:(f + 1) * C], o1[f * C:(f + 1) * C]), (name, f)
