@@ -487,36 +487,44 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
 
 constexpr int kFxThreads = 256; /* k_decode_fx: frames per workgroup (one CRC table copy) */
 constexpr int kFxGroup = 8;     /* samples per comparison group (one 16- or 32-byte source load) */
-constexpr int kFxRing = 8;      /* stream dwords a lane keeps in LDS ahead of its bit window */
+constexpr int kFxRing = 16;     /* stream dwords a lane keeps in LDS ahead of its bit window */
 
 /* k_decode_fx's reader.  Lanes read 64 unrelated frames, so a per-lane dword load that is
  * waited for at once would stall the whole wave about every sample.  Instead the window's
  * next dwords come from a per-lane LDS ring that the sample loop refills with one 16-byte
- * load per lane every 4 samples, at points common to all lanes, and commits 4 samples later
- * (the load has had those samples to land).  A lane that outruns its ring (long codes,
- * headers) reads the stream directly.
+ * load per lane every 4 samples, at points common to all lanes, and lands 8 samples later.
+ * A lane that outruns its ring (long codes, headers) reads the stream directly.
  * The window (hi, lo) is dwords k, k + 1 counted from the frame's first whole dword
- * cw = ceil(F / 4) (k starts at -1 for every frame alignment); the read position is
- * 32 (cw + k) + 32 - sh.  Ring slot j & 7 holds dword j for j in [k + 2, fe).  Dwords
+ * cw = ceil(F / 4) (k starts at -1 for every frame alignment), nx is dword k + 2 (read one
+ * dword ahead, so the ring's LDS latency is off the decode chain); the read position is
+ * 32 (cw + k) + 32 - sh.  Ring slot j & 15 holds dword j for j in [k + 3, fe).  Dwords
  * k in [0, nfold) are folded into the CRC-16 as they leave the window (decode_general's
- * cnext / cend, relative). */
+ * cnext / cend, relative; a separate wave-per-frame CRC pass measured slower). */
 struct FxReader {
     const uint32_t* wb; /* dword cw */
     int32_t nrel;       /* wb[0 .. nrel) lie inside the stream */
-    uint32_t hi, lo, crc;
-    int32_t sh, k, nfold, knear, fe; /* k >= knear: a 32-bit read could pass the stream's end */
-    uint32_t* sr;                    /* this lane's ring column: slot j at sr[j * kFxThreads] */
+    uint32_t hi, lo, nx;
+    int32_t sh, k, knear, fe, fi; /* k >= knear: a 32-bit read could pass the stream's end;
+                                     [fe, fi): dwords whose loads are in flight */
+    uint32_t* sr;                 /* this lane's ring column: slot j at sr[j * kFxThreads] */
+    uint32_t crc;                 /* CRC-16 of the frame's dwords k' in [0, min(k, nfold)) so far */
+    int32_t nfold;
     const uint16_t* ct;
-    __device__ __forceinline__ void fold(uint32_t be) {
+    __device__ __forceinline__ uint32_t direct(int32_t j) const {
+        return (uint32_t)j < (uint32_t)nrel ? __builtin_bswap32(wb[j]) : 0u;
+    }
+    __device__ __forceinline__ uint32_t folded(uint32_t be) const { /* crc after one more whole dword */
         const uint32_t v = be ^ (crc << 16);
-        crc = ct[3 * 256 + (v >> 24)] ^ ct[2 * 256 + ((v >> 16) & 0xFF)] ^ ct[256 + ((v >> 8) & 0xFF)] ^ ct[v & 0xFF];
+        return (uint32_t)ct[3 * 256 + (v >> 24)] ^ (uint32_t)ct[2 * 256 + ((v >> 16) & 0xFF)] ^
+               (uint32_t)ct[256 + ((v >> 8) & 0xFF)] ^ (uint32_t)ct[v & 0xFF];
     }
     __device__ __forceinline__ void adv() {
-        if ((uint32_t)k < (uint32_t)nfold) fold(hi);
+        if ((uint32_t)k < (uint32_t)nfold) crc = folded(hi);
         hi = lo;
+        lo = nx;
         ++k;
-        const int32_t j = k + 1;
-        lo = j < fe ? sr[(j & (kFxRing - 1)) * kFxThreads] : ((uint32_t)j < (uint32_t)nrel ? __builtin_bswap32(wb[j]) : 0u);
+        const int32_t j = k + 2;
+        nx = j < fe ? sr[(j & (kFxRing - 1)) * kFxThreads] : direct(j);
     }
     /* bits read since the frame's first whole dword, minus 32 */
     __device__ __forceinline__ int64_t rel() const { return 32 * (int64_t)k + 32 - sh; }
@@ -568,22 +576,35 @@ struct FxReader {
         }
         return (int64_t)(v >> 1) ^ -(int64_t)(v & 1);
     }
-    /* the refill pipeline: the load issued at the previous refill point lands in the ring */
-    __device__ __forceinline__ void commit(const uint4& q) {
-        sr[((fe + 0) & (kFxRing - 1)) * kFxThreads] = __builtin_bswap32(q.x);
-        sr[((fe + 1) & (kFxRing - 1)) * kFxThreads] = __builtin_bswap32(q.y);
-        sr[((fe + 2) & (kFxRing - 1)) * kFxThreads] = __builtin_bswap32(q.z);
-        sr[((fe + 3) & (kFxRing - 1)) * kFxThreads] = __builtin_bswap32(q.w);
-        fe += 4;
+    /* The refill pipeline.  Loads are started and landed unconditionally, a fixed number per
+     * block, so the compiler's wait counts are exact (a load it cannot place in the count
+     * makes it wait for every load in flight): a load that is not needed reads the CRC table
+     * and lands in the trash slot kFxRing. */
+    __device__ __forceinline__ void commit(const uint4& q, const bool valid) {
+        const int32_t j = valid ? fe : kFxRing; /* slot kFxRing + t, t < 4: trash */
+        const int32_t m = valid ? kFxRing - 1 : 0x7fffffff;
+        sr[((j + 0) & m) * kFxThreads] = __builtin_bswap32(q.x);
+        sr[((j + 1) & m) * kFxThreads] = __builtin_bswap32(q.y);
+        sr[((j + 2) & m) * kFxThreads] = __builtin_bswap32(q.z);
+        sr[((j + 3) & m) * kFxThreads] = __builtin_bswap32(q.w);
+        fe += valid ? 4 : 0;
     }
-    /* dwords [fe, fe + 4) fit the ring and the stream: start their load */
-    __device__ __forceinline__ bool issue(uint4& q) {
-        fe = fe > k + 2 ? fe : k + 2;
-        if (fe + 4 - (k + 2) > kFxRing || fe + 4 > nrel) return false;
-        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4))); /* dwords: 4-byte aligned */
-        const u32x4a4 t = *reinterpret_cast<const u32x4a4*>(wb + fe);
-        q = uint4{t.x, t.y, t.z, t.w};
+    /* a lane that read past everything loaded or in flight restarts the ring after nx (the
+     * caller drops its loads in flight) */
+    __device__ __forceinline__ bool overtaken() {
+        if (k + 3 <= fi) return false;
+        fe = fi = k + 3;
         return true;
+    }
+    /* start the load of dwords [fi, fi + 4) when they fit the ring and the stream (true), else
+     * of 16 harmless bytes at `dummy` (false) */
+    __device__ __forceinline__ bool issue(uint4& q, const void* dummy) {
+        const bool ok = fi + 4 - (k + 3) <= kFxRing && fi + 4 <= nrel;
+        typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4))); /* dwords: 4-byte aligned */
+        const u32x4a4 t = *reinterpret_cast<const u32x4a4*>(ok ? (const void*)(wb + fi) : dummy);
+        q = uint4{t.x, t.y, t.z, t.w};
+        fi += ok ? 4 : 0;
+        return ok;
     }
 };
 
@@ -622,13 +643,12 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
         const int64_t nr = a.n_words - cw;
         g.nrel = nr < 0 ? 0 : nr > 0x7fffffff ? 0x7fffffff : (int32_t)nr;
         g.hi = (cw - 1 >= 0 && cw - 1 < a.n_words) ? __builtin_bswap32(a.words[cw - 1]) : 0u;
-        g.lo = cw < a.n_words ? __builtin_bswap32(a.words[cw]) : 0u;
+        g.lo = g.direct(0);
+        g.nx = g.direct(1);
         g.sh = fo;
         g.k = -1;
-        g.fe = 1;
+        g.fe = g.fi = 2;
         g.sr = sring + lane;
-        const int64_t kn = ((a.stream_bytes * 8) >> 5) - 1 - cw;
-        g.knear = kn < -1 ? -1 : kn > 0x7fffffff ? 0x7fffffff : (int32_t)kn;
         g.ct = crct;
         g.crc = 0;
         g.nfold = 0;
@@ -637,6 +657,8 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
             g.nfold = nf < 0 ? 0 : nf > 0x7fffffff ? 0x7fffffff : (int32_t)nf;
             g.crc = crc16_more(a, crct, 0u, F, E < 4 * cw ? E : 4 * cw);
         }
+        const int64_t kn = ((a.stream_bytes * 8) >> 5) - 1 - cw;
+        g.knear = kn < -1 ? -1 : kn > 0x7fffffff ? 0x7fffffff : (int32_t)kn;
 
         /* ---- frame header (decoder.py:133-245) ---- */
         if (g.uint(15) != 0x7FFC) return false;
@@ -732,56 +754,61 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
         if (g.rel() > rend()) return false;
         int rem = 0, next = plen - order, param = 0;
         bool esc = false;
-        /* the sample loop runs in blocks of 4 samples common to the lanes of the wave; at
-         * each block the stream refill (commit the previous 16-byte load, start the next)
-         * and the source-row pipeline (commit this block's 4 samples, loaded one block
-         * earlier, into the lane's LDS slots; start the next block's load) */
+        /* the sample loop runs in blocks of 4 samples common to the lanes of the wave.  Two
+         * loads of each kind are in flight per lane, in register slots alternating by block:
+         * at block B the slot B & 1 commits the stream's oldest 16 bytes into the LDS ring and
+         * this block's 4 source-row samples into the lane's LDS slots (both loaded at block
+         * B - 2), then starts the next stream load and block B + 2's source-row load. */
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         typedef typename std::conditional<EB == 4, u32x4, u32x2>::type ExpV;
+        /* the source row's block at sample i when it lies inside the row, else the CRC table */
+        const void* dummy = a.crc_slice;
         auto exp_load = [&](int i) __attribute__((always_inline)) -> ExpV {
-            return EB == 4 ? *reinterpret_cast<const ExpV*>((const int32_t*)erow + i)
-                           : *reinterpret_cast<const ExpV*>((const int16_t*)erow + i);
+            const bool in = i + 4 <= bs;
+            const void* p2 = !in ? dummy : EB == 4 ? (const void*)((const int32_t*)erow + i) : (const void*)((const int16_t*)erow + i);
+            return *reinterpret_cast<const ExpV*>(p2);
         };
-        ExpV qe{};
-        bool einflight = false;
-        if (EB && bs >= 4) {
-            qe = exp_load(0);
-            einflight = true;
-        }
-        uint4 q;
-        bool inflight = false;
+        /* the prologue starts the loads in the loop's own order (stream, row, stream, row), so
+         * the wait counts on entering the loop match those around its back edge */
+        ExpV qe0{}, qe1{};
+        uint4 q0, q1;
+        g.overtaken();
+        bool si0 = g.issue(q0, dummy);
+        if constexpr (EB != 0) qe0 = exp_load(0);
+        bool si1 = g.issue(q1, dummy);
+        if constexpr (EB != 0) qe1 = exp_load(4);
         uint32_t bad = 0;
         bool fail = false;
-        for (int i0 = 0; i0 < bs; i0 += 4) {
-            if (inflight) g.commit(q);
-            if (EB && einflight) {
-                int32_t e[4];
-                if constexpr (EB == 4) {
-                    e[0] = (int32_t)qe[0], e[1] = (int32_t)qe[1], e[2] = (int32_t)qe[2], e[3] = (int32_t)qe[3];
-                } else {
-                    e[0] = (int32_t)(qe[0] << 16) >> 16, e[1] = (int32_t)qe[0] >> 16;
-                    e[2] = (int32_t)(qe[1] << 16) >> 16, e[3] = (int32_t)qe[1] >> 16;
-                }
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) xr[kk][lane] = e[kk];
+        auto expect_commit = [&](const ExpV& qe) __attribute__((always_inline)) {
+            int32_t e[4];
+            if constexpr (EB == 4) {
+                e[0] = (int32_t)qe[0], e[1] = (int32_t)qe[1], e[2] = (int32_t)qe[2], e[3] = (int32_t)qe[3];
+            } else {
+                e[0] = (int32_t)(qe[0] << 16) >> 16, e[1] = (int32_t)qe[0] >> 16;
+                e[2] = (int32_t)(qe[1] << 16) >> 16, e[3] = (int32_t)qe[1] >> 16;
             }
-            inflight = g.issue(q);
-            einflight = EB && i0 + 8 <= bs;
-            if (einflight) qe = exp_load(i0 + 4);
-#pragma unroll 1
-            for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) xr[kk][lane] = e[kk];
+        };
+        /* samples [i0, i0 + 4) (those below bs).  MID: a block every lane has whole and past its
+         * warm-up (i0 >= 4, i0 + 4 <= bs): no per-sample bounds, the source row from the LDS
+         * slots, and a Rice code's window advance without a branch (its next dword read from
+         * the ring, which the fast-path condition guarantees holds it). */
+        auto sample = [&](const int i0, const int kk, auto mid_t) __attribute__((always_inline)) {
+            constexpr bool MID = decltype(mid_t)::value;
+            {
                 const int i = i0 + kk;
-                if (i < bs) {
+                if (MID || i < bs) {
                     uint32_t x;
-                    if (i < order) {
+                    if (!MID && i < order) {
                         x = (uint32_t)wr[i][lane];
                     } else {
                         const uint32_t W = g.peek32();
                         const int z = __builtin_clz(W | 1u);
                         const int nb = z + 1 + param;
                         uint32_t r;
-                        if (W == 0 || nb > 32 || rem == 0 || esc || g.k >= g.knear) {
+                        if (W == 0 || nb > 32 || rem == 0 || esc || g.k >= g.knear || (MID && g.k + 3 >= g.fe)) {
                             if (rem == 0) { /* get_rice_partition (decoder.py:400-411) */
                                 rem = next;
                                 next = plen;
@@ -800,7 +827,20 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
                              * W: (W << z) >> (31 - param) = 2^param + low, so v = (z << param)
                              * + low; no read can pass the stream's end (k < knear) */
                             const uint32_t v = ((W << z) >> (31 - param)) + ((uint32_t)(z - 1) << param);
-                            g.skip(nb);
+                            if constexpr (MID) {
+                                const int32_t sh2 = g.sh - nb;
+                                const bool c = sh2 < 0;
+                                const uint32_t nn = g.sr[((g.k + 3) & (kFxRing - 1)) * kFxThreads];
+                                const uint32_t fc = g.folded(g.hi);
+                                g.crc = c && (uint32_t)g.k < (uint32_t)g.nfold ? fc : g.crc;
+                                g.hi = c ? g.lo : g.hi;
+                                g.lo = c ? g.nx : g.lo;
+                                g.nx = c ? nn : g.nx;
+                                g.k += c ? 1 : 0;
+                                g.sh = c ? sh2 + 32 : sh2;
+                            } else {
+                                g.skip(nb);
+                            }
                             r = (v >> 1) ^ (0u - (v & 1u));
                         }
                         --rem;
@@ -814,16 +854,46 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
                     if constexpr (OUT) orow[i] = (int32_t)x;
                     if constexpr (EB != 0) {
                         /* a block that ends past bs has no committed slots: the row directly */
-                        const int32_t e = i0 + 4 <= bs ? xr[kk][lane]
-                                                      : (EB == 2 ? (int32_t)((const int16_t*)erow)[i] : ((const int32_t*)erow)[i]);
+                        const int32_t e = MID || i0 + 4 <= bs ? xr[kk][lane]
+                                                              : (EB == 2 ? (int32_t)((const int16_t*)erow)[i] : ((const int32_t*)erow)[i]);
                         bad |= x ^ (uint32_t)e;
                     }
                 }
             }
+        };
+        auto block = [&](const int i0) __attribute__((always_inline)) {
+            if (__builtin_amdgcn_ballot_w64(!(i0 >= 4 && i0 + 4 <= bs)) == 0) { /* wave-uniform */
+                sample(i0, 0, std::true_type{});
+                sample(i0, 1, std::true_type{});
+                sample(i0, 2, std::true_type{});
+                sample(i0, 3, std::true_type{});
+            } else {
+#pragma unroll 1
+                for (int kk = 0; kk < 4; ++kk) sample(i0, kk, std::false_type{});
+            }
+        };
+        /* two blocks per iteration, each with its own register slot (no copies of registers
+         * whose loads are in flight: a copy would wait for them) */
+        for (int i0 = 0; i0 < bs; i0 += 8) {
+            g.commit(q0, si0);
+            if constexpr (EB != 0) expect_commit(qe0);
+            if (g.overtaken()) si1 = false;
+            si0 = g.issue(q0, dummy);
+            if constexpr (EB != 0) qe0 = exp_load(i0 + 8);
+            block(i0);
             if (fail || bad) break; /* a failed check (escape width 0, end of stream) or a difference */
+            g.commit(q1, si1);
+            if constexpr (EB != 0) expect_commit(qe1);
+            if (g.overtaken()) si0 = false;
+            si1 = g.issue(q1, dummy);
+            if constexpr (EB != 0) qe1 = exp_load(i0 + 12);
+            block(i0 + 4);
+            if (fail || bad) break;
         }
-        if (inflight) g.commit(q);
         if (fail || bad) return false;
+        /* the stream loads still in flight, oldest first */
+        g.commit(q0, si0);
+        g.commit(q1, si1);
     }
     /* ---- footer (decoder.py:124-128) ---- */
     if (g.rel() & 7) {
@@ -856,7 +926,7 @@ __global__ __launch_bounds__(kFxThreads) __attribute__((amdgpu_waves_per_eu(EB =
      * a FIXED subframe's warm-up samples (slots 0..3) and the source row's current block of 4
      * (slots 4..7); a lane is in one kind of subframe at a time */
     __shared__ int32_t ring[kFxGroup][kFxThreads];
-    __shared__ uint32_t sring[kFxRing * kFxThreads];
+    __shared__ uint32_t sring[(kFxRing + 4) * kFxThreads]; /* + the trash slots */
     __shared__ uint16_t crct[4 * 256];
     const int lane = threadIdx.x;
     for (int i = lane; i < 4 * 256; i += kFxThreads) crct[i] = a.crc_slice[i];
@@ -911,6 +981,7 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t s) {
     if (!a.defer_all && !(a.expect && !a.expect_vec) && !(a.out && (a.out_stride & 3))) {
         hipError_t e = hipMemsetAsync(a.defer_count, 0, sizeof(unsigned long long), s);
         if (e != hipSuccess) return e;
+
         const dim3 g((unsigned)((a.n_frames + kFxThreads - 1) / kFxThreads)), b(kFxThreads);
         const int eb = a.expect ? a.expect_bytes : 0;
         if (a.out) {
