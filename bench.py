@@ -324,9 +324,12 @@ def frame_writer_leg(args, cfg, az, samples, meta, rparams, residual, pstride, u
     dms = e0.elapsed_time(e1) / 2
     res["decoder_round_trip"] = {
         "ms_per_call": dms, "samples_per_s": nf * C * n / (dms * 1e-3),
+        "algorithmic_GBs": (total + nf * C * n * sbytes) / (dms * 1e-3) / 1e9,
         "frames_with_status": int((dst != 0).sum().item()), "samples_mismatched": int(dmm.sum().item()),
-        "note": "k_decode (one lane per frame) over every written frame, decoded samples compared in-kernel "
-                "with the source units; CRC-8/16, frame numbers and frame ends verified"}
+        "note": "k_decode_fx (one lane per frame: CONSTANT/VERBATIM/FIXED subframes, every check passing) "
+                "then k_decode (the general decoder) over the frames it lists, decoded samples compared "
+                "in-kernel with the source units; CRC-8/16, frame numbers and frame ends verified; "
+                "algorithmic bytes = the stream read + the source rows compared"}
     if check:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import frame_writer as FW  # checker only
