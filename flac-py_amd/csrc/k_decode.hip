@@ -486,7 +486,7 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
 }
 
 constexpr int kFxThreads = 256; /* k_decode_fx: frames per workgroup (one CRC table copy) */
-constexpr int kFxGroup = 8;     /* samples per comparison group (one 16- or 32-byte source load) */
+constexpr int kFxGroup = 4;     /* CONSTANT / VERBATIM samples between comparisons (ring slots) */
 constexpr int kFxRing = 16;     /* stream dwords a lane keeps in LDS ahead of its bit window */
 
 /* k_decode_fx's reader.  Lanes read 64 unrelated frames, so a per-lane dword load that is
@@ -581,12 +581,11 @@ struct FxReader {
      * makes it wait for every load in flight): a load that is not needed reads the CRC table
      * and lands in the trash slot kFxRing. */
     __device__ __forceinline__ void commit(const uint4& q, const bool valid) {
-        const int32_t j = valid ? fe : kFxRing; /* slot kFxRing + t, t < 4: trash */
-        const int32_t m = valid ? kFxRing - 1 : 0x7fffffff;
-        sr[((j + 0) & m) * kFxThreads] = __builtin_bswap32(q.x);
-        sr[((j + 1) & m) * kFxThreads] = __builtin_bswap32(q.y);
-        sr[((j + 2) & m) * kFxThreads] = __builtin_bswap32(q.z);
-        sr[((j + 3) & m) * kFxThreads] = __builtin_bswap32(q.w);
+        auto slot = [&](int t) { return valid ? (fe + t) & (kFxRing - 1) : kFxRing; }; /* kFxRing: trash */
+        sr[slot(0) * kFxThreads] = __builtin_bswap32(q.x);
+        sr[slot(1) * kFxThreads] = __builtin_bswap32(q.y);
+        sr[slot(2) * kFxThreads] = __builtin_bswap32(q.z);
+        sr[slot(3) * kFxThreads] = __builtin_bswap32(q.w);
         fe += valid ? 4 : 0;
     }
     /* a lane that read past everything loaded or in flight restarts the ring after nx (the
@@ -730,9 +729,12 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
          * modulo 2^32, which is what the int32 ring keeps (decode_general: int32 history). */
         const int order = t & 7;
         uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+        uint32_t wbad = 0; /* the warm-up samples are compared (and written) as they are read */
         for (int k = 0; k < order; ++k) {
             const uint32_t x = (uint32_t)g.sint(w);
-            wr[k][lane] = (int32_t)x;
+            if constexpr (OUT) orow[k] = (int32_t)x;
+            if constexpr (EB == 2) wbad |= x ^ (uint32_t)(int32_t)((const int16_t*)erow)[k];
+            if constexpr (EB == 4) wbad |= x ^ (uint32_t)((const int32_t*)erow)[k];
             const uint32_t u1 = x - d0, u2 = u1 - d1, u3 = u2 - d2;
             d0 = x;
             d1 = u1;
@@ -778,7 +780,7 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
         if constexpr (EB != 0) qe0 = exp_load(0);
         bool si1 = g.issue(q1, dummy);
         if constexpr (EB != 0) qe1 = exp_load(4);
-        uint32_t bad = 0;
+        uint32_t bad = wbad;
         bool fail = false;
         auto expect_commit = [&](const ExpV& qe) __attribute__((always_inline)) {
             int32_t e[4];
@@ -799,11 +801,9 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
             constexpr bool MID = decltype(mid_t)::value;
             {
                 const int i = i0 + kk;
-                if (MID || i < bs) {
+                if (MID || (i < bs && i >= order)) { /* warm-up samples: compared as read */
                     uint32_t x;
-                    if (!MID && i < order) {
-                        x = (uint32_t)wr[i][lane];
-                    } else {
+                    {
                         const uint32_t W = g.peek32();
                         const int z = __builtin_clz(W | 1u);
                         const int nb = z + 1 + param;
@@ -861,16 +861,45 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
                 }
             }
         };
+        /* a middle-block sample on the fast path for every lane of the wave, or false (nothing
+         * consumed) when some lane needs the general path: the block's rest then goes there */
+        auto mid_sample = [&](const int i0, const int kk) __attribute__((always_inline)) -> bool {
+            const uint32_t W = g.peek32();
+            const int z = __builtin_clz(W | 1u);
+            const int nb = z + 1 + param;
+            const bool haz = W == 0 || nb > 32 || rem == 0 || esc || g.k >= g.knear || g.k + 3 >= g.fe;
+            if (__builtin_amdgcn_ballot_w64(haz) != 0) return false; /* wave-uniform */
+            const uint32_t v = ((W << z) >> (31 - param)) + ((uint32_t)(z - 1) << param);
+            const int32_t sh2 = g.sh - nb;
+            const bool c = sh2 < 0; /* the window advances one dword (its next from the ring) */
+            const uint32_t nn = g.sr[((g.k + 3) & (kFxRing - 1)) * kFxThreads];
+            const uint32_t fc = g.folded(g.hi);
+            g.crc = c && (uint32_t)g.k < (uint32_t)g.nfold ? fc : g.crc;
+            g.hi = c ? g.lo : g.hi;
+            g.lo = c ? g.nx : g.lo;
+            g.nx = c ? nn : g.nx;
+            g.k += c ? 1 : 0;
+            g.sh = c ? sh2 + 32 : sh2;
+            const uint32_t r = (v >> 1) ^ (0u - (v & 1u));
+            --rem;
+            const uint32_t u3 = r + d3, u2 = u3 + d2, u1 = u2 + d1, x = u1 + d0;
+            d0 = m0 ? x : 0u;
+            d1 = m1 ? u1 : 0u;
+            d2 = m2 ? u2 : 0u;
+            d3 = m3 ? u3 : 0u;
+            if constexpr (OUT) orow[i0 + kk] = (int32_t)x;
+            if constexpr (EB != 0) bad |= x ^ (uint32_t)xr[kk][lane];
+            return true;
+        };
         auto block = [&](const int i0) __attribute__((always_inline)) {
+            int kk = 0;
             if (__builtin_amdgcn_ballot_w64(!(i0 >= 4 && i0 + 4 <= bs)) == 0) { /* wave-uniform */
-                sample(i0, 0, std::true_type{});
-                sample(i0, 1, std::true_type{});
-                sample(i0, 2, std::true_type{});
-                sample(i0, 3, std::true_type{});
-            } else {
-#pragma unroll 1
-                for (int kk = 0; kk < 4; ++kk) sample(i0, kk, std::false_type{});
+#pragma unroll
+                for (; kk < 4; ++kk)
+                    if (!mid_sample(i0, kk)) break;
             }
+#pragma unroll 1
+            for (; kk < 4; ++kk) sample(i0, kk, std::false_type{});
         };
         /* two blocks per iteration, each with its own register slot (no copies of registers
          * whose loads are in flight: a copy would wait for them) */
@@ -922,18 +951,17 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
 
 template <int EB, bool OUT>
 __global__ __launch_bounds__(kFxThreads) __attribute__((amdgpu_waves_per_eu(EB == 0 && !OUT ? 8 : 7, 8))) void k_decode_fx(DecodeArgs a) {
-    /* per-lane columns: a CONSTANT / VERBATIM subframe's samples between flushes (8 slots), or
-     * a FIXED subframe's warm-up samples (slots 0..3) and the source row's current block of 4
-     * (slots 4..7); a lane is in one kind of subframe at a time */
+    /* per-lane columns: a CONSTANT / VERBATIM subframe's samples between flushes, or a FIXED
+     * subframe's source-row block of 4; a lane is in one kind of subframe at a time */
     __shared__ int32_t ring[kFxGroup][kFxThreads];
-    __shared__ uint32_t sring[(kFxRing + 4) * kFxThreads]; /* + the trash slots */
+    __shared__ uint32_t sring[(kFxRing + 1) * kFxThreads]; /* + the trash slot */
     __shared__ uint16_t crct[4 * 256];
     const int lane = threadIdx.x;
     for (int i = lane; i < 4 * 256; i += kFxThreads) crct[i] = a.crc_slice[i];
     __syncthreads();
     const int64_t f = (int64_t)blockIdx.x * kFxThreads + lane;
     if (f >= a.n_frames) return;
-    if (decode_fx<EB, OUT>(a, f, ring, ring, ring + 4, sring, crct, lane)) {
+    if (decode_fx<EB, OUT>(a, f, ring, ring, ring, sring, crct, lane)) {
         a.status[f] = 0;
         a.mismatch[f] = 0;
         a.decorr[f] = 0;
