@@ -37,8 +37,8 @@ CONFIGS = {
     # configs[3]: 1e8 blocks of config 2's shape, generated on the device chunk by chunk
     # (9.2e11 bytes of PCM cannot be materialised); chunks go round-robin to the ranks and
     # one step is the whole 1e8 blocks: strong scaling, generation inside the timed region
-    "c4": dict(workload="1e8 synthetic mono 4608-sample int16 blocks generated on device in 1e6-block chunks, "
-                        "-l 12 -q 5 -r 0,5", n=4608, bits=16, L=12, q=5, rmin=0, rmax=5, mode=0,
+    "c4": dict(workload="1e8 synthetic mono 4608-sample int16 blocks generated on device in 1e6-block chunks "
+                        "(double-buffered: the next chunk generated while this one is analysed), -l 12 -q 5 -r 0,5", n=4608, bits=16, L=12, q=5, rmin=0, rmax=5, mode=0,
                units=1_000_000, channels=1, total_units=100_000_000),
     # configs[4]: fixed-only (-l 0 mode of this build) + Rice search
     "c5": dict(workload="fixed-only 4608-sample int16 blocks, -r 0,5",
@@ -469,15 +469,52 @@ def run_chunks(az, cfg, params, bufs, chunk_ids, units, total_units, seed, strea
     sbytes = samples.element_size()
     sstride, pstride, rstride = samples.shape[1], rparams.shape[1], residual.shape[1]
     bufs["stats_acc"].zero_()
-    for ci in chunk_ids:
-        cu = min(units, total_units - ci * units)
-        az.synth_device(samples.data_ptr(), sbytes, bits, sstride, ci * units, cu, n, seed, stream, open_eighths)
-        az.analyze_device(samples.data_ptr(), sbytes, bits, sstride, cu, n, params, meta.data_ptr(),
+
+    def analyse(ci, cu, rows):
+        az.analyze_device(rows.data_ptr(), sbytes, bits, sstride, cu, n, params, meta.data_ptr(),
                           rparams.data_ptr(), pstride, residual.data_ptr(), rstride, 4, stream)
         az.stream_stats(meta.data_ptr(), cu, n, bufs["stats"].data_ptr(), stream)
         bufs["stats_acc"].add_(bufs["stats"])
+        bufs["cur_samples"] = rows
         if on_chunk is not None:
             on_chunk(ci, cu)
+
+    def size(ci):
+        return min(units, total_units - ci * units)
+
+    if "samples_b" not in bufs or len(chunk_ids) < 2:
+        for ci in chunk_ids:
+            az.synth_device(samples.data_ptr(), sbytes, bits, sstride, ci * units, size(ci), n, seed, stream, open_eighths)
+            analyse(ci, size(ci), samples)
+        return bufs["stats_acc"]
+    # double-buffered (the input of a streaming encoder): chunk k + 1 is generated into the
+    # other buffer on bufs["synth_stream"] while chunk k is analysed; events order each buffer's
+    # generation after the analysis that last read it, and each analysis after its generation
+    import torch
+    main = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
+    side = bufs["synth_stream"]
+    rows = (samples, bufs["samples_b"])
+    ready = (torch.cuda.Event(), torch.cuda.Event())
+    freed = (torch.cuda.Event(), torch.cuda.Event())
+    start = torch.cuda.Event()
+    start.record(main)
+    side.wait_event(start)  # the previous step's last reads of buffer 0
+
+    def gen(k):
+        ci = chunk_ids[k]
+        az.synth_device(rows[k & 1].data_ptr(), sbytes, bits, sstride, ci * units, size(ci), n, seed,
+                        side.cuda_stream, open_eighths)
+        ready[k & 1].record(side)
+
+    gen(0)
+    for k, ci in enumerate(chunk_ids):
+        main.wait_event(ready[k & 1])
+        analyse(ci, size(ci), rows[k & 1])
+        freed[k & 1].record(main)
+        if k + 1 < len(chunk_ids):
+            if k >= 1:
+                side.wait_event(freed[(k + 1) & 1])  # chunk k - 1's analysis read that buffer
+            gen(k + 1)
     return bufs["stats_acc"]
 
 
@@ -575,6 +612,9 @@ def main(argv=None):
 
     stats_acc = torch.zeros_like(stats)
     bufs = dict(samples=samples, meta=meta, rparams=rparams, residual=residual, stats=stats, stats_acc=stats_acc)
+    if chunked and len(my_chunks) > 1:  # c4: the next chunk is generated while this one is analysed
+        bufs["samples_b"] = torch.empty_like(samples)
+        bufs["synth_stream"] = torch.cuda.Stream(dev)
     # N > 1: the stream totals go through the C-ABI collective (flacmi_allreduce_stats)
     comm, comm_note = open_stats_comm(az, dist, rank, world, dev) if distributed else (None, "")
 

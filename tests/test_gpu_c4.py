@@ -45,7 +45,7 @@ def test_c4_round_robin_chunks_equal_single_rank():
         """first, last and two random units of the chunk against the oracle"""
         torch.cuda.synchronize(dev)
         pick = sorted({0, cu - 1, *rng.integers(0, cu, 2).tolist()})
-        rows = bufs["samples"][pick].cpu().numpy()[:, :n]
+        rows = bufs.get("cur_samples", bufs["samples"])[pick].cpu().numpy()[:, :n]
         want = oracle.synth_batch(ci * CHUNK + pick[0], 1, n, bits, 2024)[0]
         assert np.array_equal(rows[0], want), f"chunk {ci}: generated block differs from the oracle's"
         ora = oracle.analyze_batch(np.ascontiguousarray(rows), oracle.make_params(cfg["L"], cfg["q"], cfg["rmin"],
@@ -81,5 +81,21 @@ def test_c4_round_robin_chunks_equal_single_rank():
             assert whole[64] == TOTAL, "config-4 units raise no exception"
         else:
             assert total.tolist() == whole.tolist(), f"W={W}: summed rank statistics differ from one rank"
+    assert checked == list(range(11))
+    # bench.py's double-buffered chunk loop (the next chunk generated on a side stream while
+    # this one is analysed): same statistics at W = 1 and 2, and every chunk's sampled units
+    # equal to the oracle
+    bufs["samples_b"] = torch.empty_like(bufs["samples"])
+    bufs["synth_stream"] = torch.cuda.Stream(dev)
+    checked.clear()
+    for W in (1, 2):
+        total = np.zeros(abi.STATS_WORDS, dtype=np.int64)
+        for r in range(W):
+            _, chunks, _ = bench.shard_plan(cfg, r, W, CHUNK, TOTAL)
+            st = bench.run_chunks(az, cfg, params, bufs, chunks, CHUNK, TOTAL, 2024, stream,
+                                  on_chunk=sample_chunk if W == 1 else None)
+            torch.cuda.synchronize(dev)
+            total += st.cpu().numpy()
+        assert total.tolist() == whole.tolist(), f"double-buffered W={W}: statistics differ"
     assert checked == list(range(11))
     az.close()
