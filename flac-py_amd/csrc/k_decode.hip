@@ -861,14 +861,16 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
                 }
             }
         };
-        /* a middle-block sample on the fast path for every lane of the wave, or false (nothing
-         * consumed) when some lane needs the general path: the block's rest then goes there */
-        auto mid_sample = [&](const int i0, const int kk) __attribute__((always_inline)) -> bool {
+        /* A middle block whose 4 samples need no partition header, escape, stream-end or ring
+         * check (tested once, at its start) decodes speculatively: each sample on the fast path,
+         * its only per-sample hazard (a code longer than the 32-bit window) collected in a lane
+         * flag.  If any lane raised it, the state saved at the block's start is restored and the
+         * general sample path redoes the block. */
+        auto mid_sample = [&](const int i0, const int kk, uint32_t& hz, uint32_t& bb) __attribute__((always_inline)) {
             const uint32_t W = g.peek32();
             const int z = __builtin_clz(W | 1u);
             const int nb = z + 1 + param;
-            const bool haz = W == 0 || nb > 32 || rem == 0 || esc || g.k >= g.knear || g.k + 3 >= g.fe;
-            if (__builtin_amdgcn_ballot_w64(haz) != 0) return false; /* wave-uniform */
+            hz |= (uint32_t)(W == 0) | (uint32_t)(nb > 32);
             const uint32_t v = ((W << z) >> (31 - param)) + ((uint32_t)(z - 1) << param);
             const int32_t sh2 = g.sh - nb;
             const bool c = sh2 < 0; /* the window advances one dword (its next from the ring) */
@@ -881,25 +883,36 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
             g.k += c ? 1 : 0;
             g.sh = c ? sh2 + 32 : sh2;
             const uint32_t r = (v >> 1) ^ (0u - (v & 1u));
-            --rem;
             const uint32_t u3 = r + d3, u2 = u3 + d2, u1 = u2 + d1, x = u1 + d0;
             d0 = m0 ? x : 0u;
             d1 = m1 ? u1 : 0u;
             d2 = m2 ? u2 : 0u;
             d3 = m3 ? u3 : 0u;
             if constexpr (OUT) orow[i0 + kk] = (int32_t)x;
-            if constexpr (EB != 0) bad |= x ^ (uint32_t)xr[kk][lane];
-            return true;
+            if constexpr (EB != 0) bb |= x ^ (uint32_t)xr[kk][lane];
         };
         auto block = [&](const int i0) __attribute__((always_inline)) {
-            int kk = 0;
-            if (__builtin_amdgcn_ballot_w64(!(i0 >= 4 && i0 + 4 <= bs)) == 0) { /* wave-uniform */
-#pragma unroll
-                for (; kk < 4; ++kk)
-                    if (!mid_sample(i0, kk)) break;
+            const bool whole = i0 >= 4 && i0 + 4 <= bs;
+            const bool calm = rem >= 4 && !esc && g.k + 3 < g.knear && g.k + 6 < g.fe;
+            if (__builtin_amdgcn_ballot_w64(!(whole && calm)) == 0) { /* wave-uniform */
+                const uint32_t s_hi = g.hi, s_lo = g.lo, s_nx = g.nx, s_crc = g.crc;
+                const int32_t s_sh = g.sh, s_k = g.k;
+                const uint32_t s_d0 = d0, s_d1 = d1, s_d2 = d2, s_d3 = d3;
+                uint32_t hz = 0, bb = 0;
+                mid_sample(i0, 0, hz, bb);
+                mid_sample(i0, 1, hz, bb);
+                mid_sample(i0, 2, hz, bb);
+                mid_sample(i0, 3, hz, bb);
+                if (__builtin_amdgcn_ballot_w64(hz != 0) == 0) {
+                    rem -= 4;
+                    bad |= bb;
+                    return;
+                }
+                g.hi = s_hi, g.lo = s_lo, g.nx = s_nx, g.crc = s_crc, g.sh = s_sh, g.k = s_k;
+                d0 = s_d0, d1 = s_d1, d2 = s_d2, d3 = s_d3;
             }
 #pragma unroll 1
-            for (; kk < 4; ++kk) sample(i0, kk, std::false_type{});
+            for (int kk = 0; kk < 4; ++kk) sample(i0, kk, std::false_type{});
         };
         /* two blocks per iteration, each with its own register slot (no copies of registers
          * whose loads are in flight: a copy would wait for them) */
