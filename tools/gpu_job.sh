@@ -2,7 +2,7 @@
 # other tools/gpu_*.sh, pmc_*.sh and profile.sh)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r6x; mkdir -p $O
+O=gpurun_out/r6y; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "frame or decode or writer or cli or encoder" > $O/pt.log 2>&1; rc=$?; tail -1 $O/pt.log; [ $rc -eq 0 ] || { grep -B5 -A30 "FAILED\|Error" $O/pt.log | head -80; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 --e2e-units 0 --no-parity > $O/b.json 2> $O/err.txt || { tail $O/err.txt; exit 1; }
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1); grep -i "decode\|k_pack32" $f | cut -c1-160
