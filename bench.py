@@ -696,7 +696,8 @@ def main(argv=None):
         extra = [rng.choice(np.nonzero(tiers_all == t)[0], size=min(8, int((tiers_all == t).sum())), replace=False)
                  for t in np.unique(tiers_all)]
         pick = np.unique(np.concatenate([pick] + extra))
-        s_host = samples[torch.as_tensor(pick, device=dev)].cpu().numpy()[:, :n]
+        rows = bufs.get("cur_samples", samples)  # c4: the buffer the last analysed chunk was generated in
+        s_host = rows[torch.as_tensor(pick, device=dev)].cpu().numpy()[:, :n]
         ora = oracle.analyze_batch(np.ascontiguousarray(s_host), oracle.make_params(cfg["L"], cfg["q"], cfg["rmin"],
                                    cfg["rmax"], cfg["mode"]), n, sample_bits=bits, threads=16)
         res_host = residual[torch.as_tensor(pick, device=dev)].cpu().numpy().view(np.uint32)

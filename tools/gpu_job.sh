@@ -2,11 +2,6 @@
 # other tools/gpu_*.sh, pmc_*.sh and profile.sh)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r6za; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "frame or writer or cli or encoder or decode" > $O/pt.log 2>&1; rc=$?; tail -1 $O/pt.log; [ $rc -eq 0 ] || { grep -B5 -A30 "FAILED\|Error" $O/pt.log | head -80; exit 1; }
-for v in cur pre cur pre; do
-  L=$PWD/flac-py_amd/libflacmi.so
-  [ $v = pre ] && L=$PWD/flac-py_amd/libflacmi_pre.so
-  FLACMI_LIB=$L timeout -k 10 300 python bench.py --steps 3 --warmup 1 --cpu-seconds 0 --e2e-units 0 > $O/b_$v.json 2> $O/err_$v.txt || { tail $O/err_$v.txt; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/b_$v.json')); f=d['frame_writer']; r=f['decoder_round_trip']; print('$v pack', round(f['ms_per_call'],3), 'decode', round(r['ms_per_call'],3), r['frames_with_status'], r['samples_mismatched'], f['parity']['mismatches'])"
-done
+O=gpurun_out/r6g2; mkdir -p $O
+timeout -k 10 400 python bench.py --config c4 --open 0 --steps 3 --warmup 1 --cpu-seconds 3 > $O/bench_c4_o0.json 2> $O/bench_c4_o0.err || { tail -20 $O/bench_c4_o0.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench_c4_o0.json'));print('c4',d['value'],d['kernels'].get('k_resid_ms'),d['roofline']['frac'],(d.get('parity') or {}).get('mismatches'),d['stream_stats']['lpc_tiers'])"
