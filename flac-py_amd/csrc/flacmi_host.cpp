@@ -874,9 +874,11 @@ int flacmi_decode_frames_device(flacmi_ctx* ctx, const uint8_t* stream_data, int
         if (expect->n_tail_units && expect->tail_len > expect->block_len) return fail(FLACMI_E_INVALID, "expect: tail_len > block_len");
     }
     if (int rc = set_device(ctx)) return rc;
-    /* workspace: decorr codes [n_frames] i32, the deferred-frame count (8 B) and list [n_frames] i64 */
+    /* workspace: decorr codes [n_frames] i32, then two deferred-frame lists (an 8 B count and
+     * [n_frames] i64 each) */
     const size_t dlist = (sizeof(int32_t) * (size_t)n_frames + 15) & ~(size_t)15;
-    if (int rc = ensure_buf(ctx->dec, dlist + 16 + sizeof(int64_t) * (size_t)n_frames)) return rc;
+    const size_t dl2 = dlist + 16 + sizeof(int64_t) * (size_t)n_frames; /* the second list */
+    if (int rc = ensure_buf(ctx->dec, dl2 + 16 + sizeof(int64_t) * (size_t)n_frames)) return rc;
     DecodeArgs a{};
     a.words = reinterpret_cast<const uint32_t*>(stream_data);
     a.stream_bytes = stream_bytes;
@@ -904,6 +906,8 @@ int flacmi_decode_frames_device(flacmi_ctx* ctx, const uint8_t* stream_data, int
     a.decorr = (int32_t*)ctx->dec.p;
     a.defer_count = (unsigned long long*)((char*)ctx->dec.p + dlist);
     a.defer_list = (int64_t*)((char*)ctx->dec.p + dlist + 16);
+    a.defer2_count = (unsigned long long*)((char*)ctx->dec.p + dl2);
+    a.defer2_list = (int64_t*)((char*)ctx->dec.p + dl2 + 16);
     a.defer_all = knob(kKnobDecodeGeneric) != 0;
     a.crc_slice = ctx->d_crc;
     HIP_TRY(launch_decode(a, (hipStream_t)stream));

@@ -125,6 +125,9 @@ struct DecodeArgs {
     unsigned long long* defer_count; /* frames k_decode_fx hands to k_decode: count, */
     int64_t* defer_list;             /* and their indices ([n_frames]) */
     int32_t defer_all;               /* knob FLACMI_DECODE_GENERIC: every frame through k_decode */
+    unsigned long long* defer2_count; /* the frames k_decode_fx's LPC pass hands on: count, */
+    int64_t* defer2_list;             /* and their indices ([n_frames]) */
+    int32_t lpc_pass;                 /* k_decode_fx's LPC pass runs (env FLACMI_DECODE_LPC=0: off) */
 };
 
 struct ResidLaunch {

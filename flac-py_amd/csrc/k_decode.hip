@@ -488,6 +488,7 @@ __global__ __launch_bounds__(kDecThreads) void k_decode(DecodeArgs a) {
 constexpr int kFxThreads = 256; /* k_decode_fx: frames per workgroup (one CRC table copy) */
 constexpr int kFxGroup = 4;     /* CONSTANT / VERBATIM samples between comparisons (ring slots) */
 constexpr int kFxRing = 16;     /* stream dwords a lane keeps in LDS ahead of its bit window */
+constexpr int kFxLpc = 12;      /* the second pass's largest LPC order (history in registers) */
 
 /* k_decode_fx's reader.  Lanes read 64 unrelated frames, so a per-lane dword load that is
  * waited for at once would stall the whole wave about every sample.  Instead the window's
@@ -626,10 +627,10 @@ __device__ __forceinline__ bool fx_part(int32_t (*ring)[kFxThreads], const int l
  * it again from its first byte.  The checks are decode_general's, in its order, so a frame
  * this function accepts is one decode_general gives status 0 (it never reports a failure
  * itself). */
-template <int EB, bool OUT>
+template <int EB, bool OUT, int LN>
 __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, int32_t (*ring)[kFxThreads],
                                           int32_t (*wr)[kFxThreads], int32_t (*xr)[kFxThreads], uint32_t* sring,
-                                          const uint16_t* crct, const int lane) {
+                                          const uint16_t* crct, const int lane, bool& to_lpc) {
     FxReader g;
     int bs, nch, ss;
     /* the stream's last bit, relative as rel() (derived from wb: not kept in registers) */
@@ -710,7 +711,14 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
         int32_t* orow = OUT ? a.out + u * a.out_stride : nullptr;
         if (g.uint(1) != 0) return false;
         const int t = g.uint(6);
-        if (!(t <= 1 || (t >= 8 && t <= 12))) return false; /* LPC (and invalid types): k_decode */
+        /* LPC (LN > 0: orders up to LN) and invalid types: k_decode */
+        if (!(t <= 1 || (t >= 8 && t <= 12) || (LN > 0 && t >= 32 && (t & 31) < LN))) {
+            /* worth the LPC pass: measured on 16-bit streams (config 2 open mixes 36.6 -> 25.4 ms);
+             * on config 3's open mix (24-bit stereo, L 32) it cost 103 -> 116 ms, so wider
+             * samples go straight to k_decode */
+            to_lpc = LN == 0 && t >= 32 && (t & 31) < kFxLpc && ss <= 16;
+            return false;
+        }
         if (g.uint(1)) return false;                        /* wasted bits: k_decode */
         const int w = ss;
         if (t <= 1) {
@@ -727,7 +735,17 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
          * running differences: with d_j = Delta^j x[i-1], Delta^k x[i] = r and Delta^j x[i] =
          * Delta^(j+1) x[i] + d_j.  Wrapping 32-bit arithmetic gives the reference's value
          * modulo 2^32, which is what the int32 ring keeps (decode_general: int32 history). */
-        const int order = t & 7;
+        /* LPC (LN > 0, order <= LN): the last LN samples h[0] = x[i-1] .. and the quantised
+         * coefficients in registers (static indices: every loop over them is unrolled to LN);
+         * x[i] = r + (sum c_j h_j >> shift), the sum in int64 over the int32 history as
+         * decode_general's ring (decoder.py:490-498) */
+        const bool lpc = LN > 0 && t >= 32;
+        const int order = lpc ? (t & 31) + 1 : t & 7;
+        uint32_t h[LN > 0 ? LN : 1];
+        int32_t cf[LN > 0 ? LN : 1];
+        int shift = 0;
+#pragma unroll
+        for (int j = 0; j < (LN > 0 ? LN : 1); ++j) h[j] = 0, cf[j] = 0;
         uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
         uint32_t wbad = 0; /* the warm-up samples are compared (and written) as they are read */
         for (int k = 0; k < order; ++k) {
@@ -740,9 +758,25 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
             d1 = u1;
             d2 = u2;
             d3 = u3;
+            if constexpr (LN > 0) {
+#pragma unroll
+                for (int j = LN - 1; j > 0; --j) h[j] = h[j - 1];
+                h[0] = x;
+            }
+        }
+        if constexpr (LN > 0) {
+            if (lpc) { /* decoder.py:286-300: precision, shift, coefficients */
+                const int prec = g.uint(4);
+                if (prec == 15) return false;
+                shift = (int)g.sint(5);
+                if (shift < 0) return false; /* decode_general reports it after the frame */
+#pragma unroll
+                for (int j = 0; j < LN; ++j) cf[j] = j < order ? (int32_t)g.sint(prec + 1) : 0;
+                d0 = d1 = d2 = d3 = 0;
+            }
         }
         /* the levels the order uses, as lane masks (v_cndmask on SGPR pairs, no VGPRs) */
-        const bool m0 = order > 0, m1 = order > 1, m2 = order > 2, m3 = order > 3;
+        const bool m0 = !lpc && order > 0, m1 = !lpc && order > 1, m2 = !lpc && order > 2, m3 = !lpc && order > 3;
         d0 = m0 ? d0 : 0u;
         d1 = m1 ? d1 : 0u;
         d2 = m2 ? d2 : 0u;
@@ -792,6 +826,27 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
             }
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) xr[kk][lane] = e[kk];
+        };
+        /* x[i] from its residual: FIXED by the running differences, LPC by the history */
+        auto restore = [&](const uint32_t r) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (LN > 0) {
+                if (lpc) {
+                    int64_t acc = 0;
+#pragma unroll
+                    for (int j = 0; j < LN; ++j) acc += (int64_t)cf[j] * (int64_t)(int32_t)h[j];
+                    const uint32_t x = r + (uint32_t)(acc >> shift);
+#pragma unroll
+                    for (int j = LN - 1; j > 0; --j) h[j] = h[j - 1];
+                    h[0] = x;
+                    return x;
+                }
+            }
+            const uint32_t u3 = r + d3, u2 = u3 + d2, u1 = u2 + d1, x = u1 + d0;
+            d0 = m0 ? x : 0u;
+            d1 = m1 ? u1 : 0u;
+            d2 = m2 ? u2 : 0u;
+            d3 = m3 ? u3 : 0u;
+            return x;
         };
         /* samples [i0, i0 + 4) (those below bs).  MID: a block every lane has whole and past its
          * warm-up (i0 >= 4, i0 + 4 <= bs): no per-sample bounds, the source row from the LDS
@@ -844,12 +899,7 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
                             r = (v >> 1) ^ (0u - (v & 1u));
                         }
                         --rem;
-                        const uint32_t u3 = r + d3, u2 = u3 + d2, u1 = u2 + d1;
-                        x = u1 + d0;
-                        d0 = m0 ? x : 0u;
-                        d1 = m1 ? u1 : 0u;
-                        d2 = m2 ? u2 : 0u;
-                        d3 = m3 ? u3 : 0u;
+                        x = restore(r);
                     }
                     if constexpr (OUT) orow[i] = (int32_t)x;
                     if constexpr (EB != 0) {
@@ -883,11 +933,7 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
             g.k += c ? 1 : 0;
             g.sh = c ? sh2 + 32 : sh2;
             const uint32_t r = (v >> 1) ^ (0u - (v & 1u));
-            const uint32_t u3 = r + d3, u2 = u3 + d2, u1 = u2 + d1, x = u1 + d0;
-            d0 = m0 ? x : 0u;
-            d1 = m1 ? u1 : 0u;
-            d2 = m2 ? u2 : 0u;
-            d3 = m3 ? u3 : 0u;
+            const uint32_t x = restore(r);
             if constexpr (OUT) orow[i0 + kk] = (int32_t)x;
             if constexpr (EB != 0) bb |= x ^ (uint32_t)xr[kk][lane];
         };
@@ -898,6 +944,11 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
                 const uint32_t s_hi = g.hi, s_lo = g.lo, s_nx = g.nx, s_crc = g.crc;
                 const int32_t s_sh = g.sh, s_k = g.k;
                 const uint32_t s_d0 = d0, s_d1 = d1, s_d2 = d2, s_d3 = d3;
+                uint32_t s_h[LN > 0 ? LN : 1];
+                if constexpr (LN > 0) {
+#pragma unroll
+                    for (int j = 0; j < LN; ++j) s_h[j] = h[j];
+                }
                 uint32_t hz = 0, bb = 0;
                 mid_sample(i0, 0, hz, bb);
                 mid_sample(i0, 1, hz, bb);
@@ -910,6 +961,10 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
                 }
                 g.hi = s_hi, g.lo = s_lo, g.nx = s_nx, g.crc = s_crc, g.sh = s_sh, g.k = s_k;
                 d0 = s_d0, d1 = s_d1, d2 = s_d2, d3 = s_d3;
+                if constexpr (LN > 0) {
+#pragma unroll
+                    for (int j = 0; j < LN; ++j) h[j] = s_h[j];
+                }
             }
 #pragma unroll 1
             for (int kk = 0; kk < 4; ++kk) sample(i0, kk, std::false_type{});
@@ -962,7 +1017,9 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
     return true;
 }
 
-template <int EB, bool OUT>
+/* LN = 0: every frame; LN > 0: the frames the LN = 0 pass listed (defer_list), FIXED and LPC
+ * subframes of order <= LN, listing what it cannot vouch for in defer2_list */
+template <int EB, bool OUT, int LN>
 __global__ __launch_bounds__(kFxThreads) __attribute__((amdgpu_waves_per_eu(EB == 0 && !OUT ? 8 : 7, 8))) void k_decode_fx(DecodeArgs a) {
     /* per-lane columns: a CONSTANT / VERBATIM subframe's samples between flushes, or a FIXED
      * subframe's source-row block of 4; a lane is in one kind of subframe at a time */
@@ -972,15 +1029,20 @@ __global__ __launch_bounds__(kFxThreads) __attribute__((amdgpu_waves_per_eu(EB =
     const int lane = threadIdx.x;
     for (int i = lane; i < 4 * 256; i += kFxThreads) crct[i] = a.crc_slice[i];
     __syncthreads();
-    const int64_t f = (int64_t)blockIdx.x * kFxThreads + lane;
-    if (f >= a.n_frames) return;
-    if (decode_fx<EB, OUT>(a, f, ring, ring, ring, sring, crct, lane)) {
+    const int64_t kf = (int64_t)blockIdx.x * kFxThreads + lane;
+    if (kf >= (LN > 0 ? (int64_t)*a.defer_count : a.n_frames)) return;
+    const int64_t f = LN > 0 ? a.defer_list[kf] : kf;
+    bool to_lpc = false;
+    if (decode_fx<EB, OUT, LN>(a, f, ring, ring, ring, sring, crct, lane, to_lpc)) {
         a.status[f] = 0;
         a.mismatch[f] = 0;
         a.decorr[f] = 0;
     } else {
-        const unsigned long long k = atomicAdd(a.defer_count, 1ull);
-        a.defer_list[k] = f;
+        /* the first pass lists a frame for the LPC pass only when an LPC subframe of order <= kFxLpc
+         * stopped it; anything else goes straight to k_decode's list */
+        const bool l1 = LN == 0 && to_lpc && a.lpc_pass;
+        const unsigned long long k = atomicAdd(l1 ? a.defer_count : a.defer2_count, 1ull);
+        (l1 ? a.defer_list : a.defer2_list)[k] = f;
     }
 }
 
@@ -1025,16 +1087,30 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t s) {
 
         const dim3 g((unsigned)((a.n_frames + kFxThreads - 1) / kFxThreads)), b(kFxThreads);
         const int eb = a.expect ? a.expect_bytes : 0;
-        if (a.out) {
-            if (eb == 2) hipLaunchKernelGGL((k_decode_fx<2, true>), g, b, 0, s, a);
-            else if (eb == 4) hipLaunchKernelGGL((k_decode_fx<4, true>), g, b, 0, s, a);
-            else hipLaunchKernelGGL((k_decode_fx<0, true>), g, b, 0, s, a);
-        } else {
-            if (eb == 2) hipLaunchKernelGGL((k_decode_fx<2, false>), g, b, 0, s, a);
-            else if (eb == 4) hipLaunchKernelGGL((k_decode_fx<4, false>), g, b, 0, s, a);
-            else hipLaunchKernelGGL((k_decode_fx<0, false>), g, b, 0, s, a);
-        }
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        auto fx = [&](auto ln) {
+            constexpr int LN = decltype(ln)::value;
+            if (a.out) {
+                if (eb == 2) hipLaunchKernelGGL((k_decode_fx<2, true, LN>), g, b, 0, s, a);
+                else if (eb == 4) hipLaunchKernelGGL((k_decode_fx<4, true, LN>), g, b, 0, s, a);
+                else hipLaunchKernelGGL((k_decode_fx<0, true, LN>), g, b, 0, s, a);
+            } else {
+                if (eb == 2) hipLaunchKernelGGL((k_decode_fx<2, false, LN>), g, b, 0, s, a);
+                else if (eb == 4) hipLaunchKernelGGL((k_decode_fx<4, false, LN>), g, b, 0, s, a);
+                else hipLaunchKernelGGL((k_decode_fx<0, false, LN>), g, b, 0, s, a);
+            }
+            return hipGetLastError();
+        };
+        /* the listed frames again, with LPC subframes of order <= kFxLpc; the rest for k_decode */
+        static const bool lpc_pass = [] {
+            const char* v = getenv("FLACMI_DECODE_LPC");
+            return !(v && v[0] == '0');
+        }();
+        a.lpc_pass = lpc_pass;
+        if ((e = hipMemsetAsync(a.defer2_count, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
+        if ((e = fx(std::integral_constant<int, 0>{})) != hipSuccess) return e;
+        if (lpc_pass && (e = fx(std::integral_constant<int, kFxLpc>{})) != hipSuccess) return e;
+        a.defer_count = a.defer2_count;
+        a.defer_list = a.defer2_list;
         blocks = blocks < 2048 ? blocks : 2048; /* the listed frames: a grid-stride loop */
     } else {
         a.defer_all = 1; /* rows k_decode_fx cannot read with 16-byte accesses: every frame general */
