@@ -489,6 +489,7 @@ constexpr int kFxThreads = 256; /* k_decode_fx: frames per workgroup (one CRC ta
 constexpr int kFxGroup = 4;     /* CONSTANT / VERBATIM samples between comparisons (ring slots) */
 constexpr int kFxRing = 16;     /* stream dwords a lane keeps in LDS ahead of its bit window */
 constexpr int kFxLpc = 12;      /* the second pass's largest LPC order (history in registers) */
+constexpr int kFxLpcW = 32;     /* ... for samples wider than 16 bits (that pass: no speculative blocks) */
 
 /* k_decode_fx's reader.  Lanes read 64 unrelated frames, so a per-lane dword load that is
  * waited for at once would stall the whole wave about every sample.  Instead the window's
@@ -716,7 +717,7 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
             /* worth the LPC pass: measured on 16-bit streams (config 2 open mixes 36.6 -> 25.4 ms);
              * on config 3's open mix (24-bit stereo, L 32) it cost 103 -> 116 ms, so wider
              * samples go straight to k_decode */
-            to_lpc = LN == 0 && t >= 32 && (t & 31) < kFxLpc && ss <= 16;
+            to_lpc = LN == 0 && t >= 32 && (t & 31) < (a.sample_size <= 16 ? kFxLpc : kFxLpcW);
             return false;
         }
         if (g.uint(1)) return false;                        /* wasted bits: k_decode */
@@ -940,7 +941,7 @@ __device__ __forceinline__ bool decode_fx(const DecodeArgs& a, const int64_t f, 
         auto block = [&](const int i0) __attribute__((always_inline)) {
             const bool whole = i0 >= 4 && i0 + 4 <= bs;
             const bool calm = rem >= 4 && !esc && g.k + 3 < g.knear && g.k + 6 < g.fe;
-            if (__builtin_amdgcn_ballot_w64(!(whole && calm)) == 0) { /* wave-uniform */
+            if (LN <= kFxLpc && __builtin_amdgcn_ballot_w64(!(whole && calm)) == 0) { /* wave-uniform */
                 const uint32_t s_hi = g.hi, s_lo = g.lo, s_nx = g.nx, s_crc = g.crc;
                 const int32_t s_sh = g.sh, s_k = g.k;
                 const uint32_t s_d0 = d0, s_d1 = d1, s_d2 = d2, s_d3 = d3;
@@ -1108,7 +1109,10 @@ hipError_t launch_decode(DecodeArgs a, hipStream_t s) {
         a.lpc_pass = lpc_pass;
         if ((e = hipMemsetAsync(a.defer2_count, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
         if ((e = fx(std::integral_constant<int, 0>{})) != hipSuccess) return e;
-        if (lpc_pass && (e = fx(std::integral_constant<int, kFxLpc>{})) != hipSuccess) return e;
+        if (lpc_pass) {
+            e = a.sample_size <= 16 ? fx(std::integral_constant<int, kFxLpc>{}) : fx(std::integral_constant<int, kFxLpcW>{});
+            if (e != hipSuccess) return e;
+        }
         a.defer_count = a.defer2_count;
         a.defer_list = a.defer2_list;
         blocks = blocks < 2048 ? blocks : 2048; /* the listed frames: a grid-stride loop */
