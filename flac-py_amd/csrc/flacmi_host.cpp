@@ -208,7 +208,8 @@ struct KnobDef {
     const char* name;
     int dflt;
 };
-constexpr KnobDef kKnobs[kKnobCount] = {{"FLACMI_OVERLAP", -1}, {"FLACMI_MF8_GRID", 0}, {"FLACMI_STREAM_GENERIC", 0}, {"FLACMI_DECODE_GENERIC", 0}};
+constexpr KnobDef kKnobs[kKnobCount] = {{"FLACMI_OVERLAP", -1}, {"FLACMI_MF8_GRID", 0}, {"FLACMI_STREAM_GENERIC", 0}, {"FLACMI_DECODE_GENERIC", 0},
+                                        {"FLACMI_PACK_GENERIC", 0}};
 std::atomic<int> g_knob[kKnobCount];
 std::once_flag g_knob_once;
 void knobs_init() {

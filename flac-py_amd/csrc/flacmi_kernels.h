@@ -141,7 +141,7 @@ ResidLaunch resid_launch_config(int n, int rmax_eff, int residual_bytes);
 constexpr int kMaxFinestParts = 4096;
 
 /* flacmi_set_knob's knobs: the environment's value (read once) or the last value set */
-enum Knob { kKnobOverlap = 0, kKnobMf8Grid, kKnobStreamGeneric, kKnobDecodeGeneric, kKnobCount };
+enum Knob { kKnobOverlap = 0, kKnobMf8Grid, kKnobStreamGeneric, kKnobDecodeGeneric, kKnobPackGeneric, kKnobCount };
 int knob(Knob k);
 
 hipError_t launch_lpc(const LpcArgs& a, hipStream_t s);

@@ -768,9 +768,15 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
             bnd[j] = 1 << 30;
             if (k < k1) {
                 uint4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
-                if (!(a.ablate & 32)) { /* ablation 32: no residual loads (timing only) */
+                if (a.ablate & 32) { /* ablation 32: no residual loads (timing only) */
+                } else if (i0 + 8 <= n) {
                     v0 = *reinterpret_cast<const uint4*>(zrow + i0);
                     v1 = *reinterpret_cast<const uint4*>(zrow + i0 + 4);
+                } else { /* the row's last chunk: no reads past its end */
+                    v0 = uint4{zrow[i0], i0 + 1 < n ? zrow[i0 + 1] : 0u, i0 + 2 < n ? zrow[i0 + 2] : 0u,
+                               i0 + 3 < n ? zrow[i0 + 3] : 0u};
+                    v1 = uint4{i0 + 4 < n ? zrow[i0 + 4] : 0u, i0 + 5 < n ? zrow[i0 + 5] : 0u,
+                               i0 + 6 < n ? zrow[i0 + 6] : 0u, i0 + 7 < n ? zrow[i0 + 7] : 0u};
                 }
                 if (j == 0 && c == 0 && (a.ablate & 128)) v0.x ^= touch; /* never set: keeps the touch load */
                 z[j][0] = v0.x; z[j][1] = v0.y; z[j][2] = v0.z; z[j][3] = v0.w;
@@ -950,6 +956,376 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
     }
 }
 
+/* ====================================================================================
+ * k_packw: the frame writer for frames of more than kMaxC chunks a thread (config 3's
+ * 16384-sample stereo frames, 89 KB each; 32-bit residuals, partitions of >= 8 values).
+ *
+ * k_pack32's placement run tile after tile: a tile is NT * MAXC chunks, one workgroup scan
+ * gives each thread the bit position of its contiguous run, and every code is ORed into
+ * LDS at its bit position.  The LDS window is a ring of kWinWords words; window bit 0 is
+ * the 16-byte aligned output address at or below the frame's first byte.  Bits below a
+ * segment's end (the frame header, a subframe's header fields, a tile) are final, so after
+ * each segment the whole kRingChunk-word chunks below it leave the ring: thread t takes
+ * words 2t and 2t+1 of the chunk (one 8-byte LDS read, one 8-byte store, zeroed behind),
+ * folds their CRC-16 and adds it to its own running CRC multiplied by x^(8 * 2048) (the
+ * chunk length; one table in LDS).  At the frame's end a lane tree turns the 256 running
+ * CRCs into the CRC of everything that left, k_pack32's end fold takes the last < 512
+ * words, and the two are joined with one x^(8d) multiplication.  A segment that would
+ * overrun the ring writes what fits (ORs outside [fl, fl + kWinWords) are skipped), the
+ * full ring leaves, and the segment runs again: ORs are idempotent.  The general k_pack
+ * flushes a whole window at a time with a per-thread x^(8d) shift from global tables (17
+ * dependent loads a flush) and one-value-at-a-time accumulators; this kernel is its
+ * replacement for the frames it takes (the rest go to k_pack by list).
+ * ==================================================================================== */
+constexpr uint32_t kRingMask = kWinWords - 1;
+constexpr int kRingChunk = 2 * kPackThreads; /* words leaving the ring together: 2048 bytes */
+constexpr int kRingChunkLevel = 11;          /* x^(8 * 2^11) */
+
+__device__ __forceinline__ bool packw_frame_ok(const FrameArgs& a, int64_t f) {
+    for (int c = 0; c < a.channels; ++c) {
+        const int64_t u = f * a.channels + c;
+        if ((unit_len(a, u) >> a.meta[u].part_order) < 8) return false;
+    }
+    return true;
+}
+
+__device__ __forceinline__ uint32_t crc_fold_word(uint32_t c, uint32_t w, const uint16_t* ct) {
+    return (uint32_t)ct[3 * 256 + ((c >> 8) ^ (w >> 24))] ^ (uint32_t)ct[2 * 256 + ((c ^ (w >> 16)) & 0xFF)] ^
+           (uint32_t)ct[256 + ((w >> 8) & 0xFF)] ^ (uint32_t)ct[w & 0xFF];
+}
+
+template <int MAXC>
+__global__ __launch_bounds__(kPackThreads) void k_packw(FrameArgs a) {
+    constexpr int NT = kPackThreads; /* the launch uses exactly this many threads */
+    __shared__ __align__(16) uint32_t win[kWinWords];
+    __shared__ __align__(16) uint16_t ct[4 * 256];
+    __shared__ __align__(16) uint16_t pwc[512]; /* c -> c * x^(8 * kRingChunk * 4) */
+    __shared__ uint8_t hdr[16];
+    __shared__ uint32_t sub_start[9];
+    __shared__ int32_t cnt14[8];
+    __shared__ uint32_t red[NT / 64];
+    __shared__ uint32_t red2[NT / 64];
+    __shared__ int hb_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t f = blockIdx.x;
+    if (a.offsets[a.n_frames] > a.capacity) return; /* k_pack reports it */
+    if (a.status[f] != 0) return;
+    if (!packw_frame_ok(a, f)) { /* k_pack writes it */
+        if (tid == 0) a.slow_list[atomicAdd(a.slow_count, 1ull)] = f;
+        return;
+    }
+    const int64_t F = a.offsets[f], Fend = a.offsets[f + 1];
+    const int64_t lead = (int64_t)(((uintptr_t)a.out + (uintptr_t)F) & 15);
+    const int64_t Fa = F - lead;            /* output byte of window bit 0 (16-byte aligned) */
+    const uint32_t A = (uint32_t)(8 * lead); /* window bit of the frame's first bit */
+    const int64_t u0 = f * a.channels;
+    const int C = a.channels;
+    const uint16_t* __restrict__ pw = a.crc_pow;
+    for (int i = tid; i < 128; i += NT) reinterpret_cast<uint4*>(ct)[i] = reinterpret_cast<const uint4*>(a.crc_slice)[i];
+    for (int i = tid; i < 64; i += NT)
+        reinterpret_cast<uint4*>(pwc)[i] = reinterpret_cast<const uint4*>(pw + kRingChunkLevel * 512)[i];
+    for (int i = tid; i < kWinWords / 4; i += NT) reinterpret_cast<uint4*>(win)[i] = uint4{0, 0, 0, 0};
+    if (tid < 8) cnt14[tid] = 0;
+    if (tid == 0) hb_s = frame_header(a.first_frame + f, unit_len(a, u0), hdr);
+    __syncthreads();
+    for (int c = 0; c < C; ++c) {
+        const flacmi_unit_meta& m = a.meta[u0 + c];
+        if (m.coding_method == 5) {
+            const int32_t* rp = a.rice_params + (u0 + c) * a.params_stride;
+            int cnt = 0;
+            for (int k = tid; k < m.n_parts; k += NT) cnt += rp[k] > 14 ? 1 : 0;
+            if (cnt) atomicAdd(&cnt14[c], cnt);
+        }
+    }
+    __syncthreads();
+    const int hb = hb_s;
+    if (tid == 0) {
+        uint32_t s = A + 8u * (uint32_t)hb;
+        for (int c = 0; c < C; ++c) {
+            const flacmi_unit_meta& m = a.meta[u0 + c];
+            sub_start[c] = s;
+            s += sub_prefix_bits(m, a.sample_size, a.q) + (uint32_t)sub_residual_bits(m, cnt14[c]);
+        }
+        sub_start[C] = s;
+    }
+    __syncthreads();
+
+    uint32_t fl = 0;    /* ring words below fl have left (uniform) */
+    uint32_t crc_t = 0; /* this thread's running CRC over its words of the chunks that left */
+    /* the w-bit field val (1 <= w <= 32) at window bit P: one or two ORs, words outside the
+     * ring's span skipped */
+    auto ring_or = [&](uint32_t P, uint32_t val, uint32_t w) __attribute__((always_inline)) {
+        const uint64_t t = (uint64_t)val << (64u - (P & 31u) - w);
+        const uint32_t wi = P >> 5;
+        if (wi - fl < (uint32_t)kWinWords) atomicOr(&win[wi & kRingMask], (uint32_t)(t >> 32));
+        if (wi + 1u - fl < (uint32_t)kWinWords) atomicOr(&win[(wi + 1u) & kRingMask], (uint32_t)t);
+    };
+    /* whole chunks below ring word upto leave: CRC share, store, zero; frame bytes are
+     * [fb0, fb1) in window bytes */
+    const uint32_t fb0 = (uint32_t)lead, fb1 = (uint32_t)(lead + (Fend - F));
+    uint8_t* __restrict__ ob = a.out + Fa; /* output byte of window byte 0 (never written below F) */
+    auto store8 = [&](uint32_t rb, uint2 w) __attribute__((always_inline)) {
+        if (rb >= fb0 && rb + 8u <= fb1) {
+            *reinterpret_cast<uint2*>(ob + rb) = uint2{__builtin_bswap32(w.x), __builtin_bswap32(w.y)};
+        } else {
+#pragma unroll 1
+            for (uint32_t j = 0; j < 8; ++j) {
+                const uint32_t wj = j < 4 ? w.x : w.y;
+                if (rb + j >= fb0 && rb + j < fb1) ob[rb + j] = (uint8_t)(wj >> (24 - 8 * (j & 3)));
+            }
+        }
+    };
+    auto leave = [&](uint32_t upto) __attribute__((always_inline)) {
+        if (upto - fl < (uint32_t)kRingChunk) return;
+        do {
+            const uint32_t k = fl + 2u * (uint32_t)tid;
+            uint2* wp = reinterpret_cast<uint2*>(&win[k & kRingMask]);
+            const uint2 w = *wp;
+            *wp = uint2{0, 0};
+            const uint32_t c = crc_fold_word(crc_fold_word(0, w.x, ct), w.y, ct);
+            crc_t = ((uint32_t)pwc[crc_t & 0xFF] ^ (uint32_t)pwc[256 + (crc_t >> 8)]) ^ c;
+            store8(4u * k, w);
+            fl += (uint32_t)kRingChunk;
+        } while (upto - fl >= (uint32_t)kRingChunk);
+        __syncthreads(); /* zeroed words are written again by the next segment */
+    };
+
+    /* the frame header and a subframe's header fields (< 1600 bits) always fit the ring
+     * above the < kRingChunk words still waiting */
+    if (tid < hb) ring_or(A + 8u * tid, hdr[tid], 8);
+    __syncthreads();
+    leave((A + 8u * hb) >> 5);
+    const int ss = a.sample_size, q = a.q;
+    for (int c = 0; c < C; ++c) {
+        const int64_t u = u0 + c;
+        const flacmi_unit_meta& m = a.meta[u];
+        const int n = unit_len(a, u);
+        const int order = m.order, ncoefs = m.ncoefs, method = m.coding_method;
+        const bool lpc = m.kind == FLACMI_KIND_LPC;
+        const uint32_t s0 = sub_start[c];
+        const uint32_t pre = sub_prefix_bits(m, ss, q);
+        const int nfields = 1 + order + (lpc ? 2 + ncoefs : 0) + 2;
+        {
+            for (int t = tid; t < nfields; t += NT) {
+                uint32_t pos, v, w;
+                const uint32_t b = s0 + 8 + (uint32_t)order * ss;
+                const int t2 = t - 1 - order;
+                if (t == 0) {
+                    pos = s0;
+                    v = lpc ? (uint32_t)((0x20 | (order - 1)) << 1) : (uint32_t)((0x08 | order) << 1);
+                    w = 8;
+                } else if (t <= order) {
+                    const int j = t - 1;
+                    const int32_t x = a.sample_bytes == 2 ? (int32_t)((const int16_t*)a.samples)[u * a.stride + j]
+                                                          : ((const int32_t*)a.samples)[u * a.stride + j];
+                    pos = s0 + 8 + (uint32_t)j * ss;
+                    v = (uint32_t)x & (ss == 32 ? ~0u : ((1u << ss) - 1u));
+                    w = (uint32_t)ss;
+                } else if (lpc && t2 == 0) {
+                    pos = b;
+                    v = (uint32_t)((q - 1) & 15);
+                    w = 4;
+                } else if (lpc && t2 == 1) {
+                    pos = b + 4;
+                    v = (uint32_t)(m.shift & 31);
+                    w = 5;
+                } else if (lpc && t2 < 2 + ncoefs) {
+                    const int j = t2 - 2;
+                    pos = b + 9 + (uint32_t)j * q;
+                    v = (uint32_t)m.coefs[j] & ((1u << q) - 1u);
+                    w = (uint32_t)q;
+                } else {
+                    const int t3 = t2 - (lpc ? 2 + ncoefs : 0);
+                    const uint32_t b2 = b + (lpc ? 9u + (uint32_t)ncoefs * q : 0u);
+                    pos = t3 == 0 ? b2 : b2 + 2;
+                    v = t3 == 0 ? (method == 5 ? 1u : 0u) : (uint32_t)(m.part_order & 15);
+                    w = t3 == 0 ? 2u : 4u;
+                }
+                ring_or(pos, v, w);
+            }
+        }
+        __syncthreads();
+        leave((s0 + pre) >> 5);
+        /* residual: tiles of NT * MAXC chunks, thread t's run [k0, k1) of each */
+        const int ps = n >> m.part_order;
+        const int32_t* __restrict__ rp = a.rice_params + u * a.params_stride;
+        const uint32_t* __restrict__ zrow = reinterpret_cast<const uint32_t*>(a.residual) + u * a.residual_stride;
+        const int nch = (n + 7) >> 3;
+        const uint32_t pmask_m = (1u << method) - 1u;
+        uint32_t tile_base = s0 + pre;
+        for (int tb = 0; tb < nch; tb += NT * MAXC) {
+            const int k0 = tb + tid * MAXC, k1 = min(k0 + MAXC, nch);
+            uint32_t z[MAXC][8];
+            int pa[MAXC], pb[MAXC], bnd[MAXC], pt0[MAXC];
+            uint32_t tsum = 0;
+#pragma unroll
+            for (int j = 0; j < MAXC; ++j) {
+                const int k = k0 + j;
+                const int i0 = 8 * k;
+                pa[j] = pb[j] = 0;
+                bnd[j] = 1 << 30;
+                pt0[j] = 0;
+                if (k < k1) {
+                    if (i0 + 8 <= n) {
+                        const uint4 v0 = *reinterpret_cast<const uint4*>(zrow + i0);
+                        const uint4 v1 = *reinterpret_cast<const uint4*>(zrow + i0 + 4);
+                        z[j][0] = v0.x; z[j][1] = v0.y; z[j][2] = v0.z; z[j][3] = v0.w;
+                        z[j][4] = v1.x; z[j][5] = v1.y; z[j][6] = v1.z; z[j][7] = v1.w;
+                    } else { /* the row's last chunk: no reads past its end */
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) z[j][e] = i0 + e < n ? zrow[i0 + e] : 0u;
+                    }
+                    const int part0 = i0 / ps;
+                    pt0[j] = part0;
+                    const int b1 = (part0 + 1) * ps;
+                    pa[j] = rp[part0];
+                    pb[j] = (b1 < n && b1 <= i0 + 7) ? rp[part0 + 1] : pa[j];
+                    bnd[j] = b1;
+                    if (i0 > order && i0 + 8 <= n && b1 >= i0 + 8) {
+                        const int p = pa[j];
+                        uint32_t qs = 0;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) qs += z[j][e] >> p;
+                        tsum += qs + 8u * (uint32_t)(p + 1) + (i0 == part0 * ps ? (uint32_t)method : 0u);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            const int i = i0 + e;
+                            const int p = i >= b1 ? pb[j] : pa[j];
+                            const bool valid = i >= order && i < n;
+                            const bool first = i == order || (i > order && (i == b1 || i == part0 * ps));
+                            tsum += valid ? (first ? (uint32_t)method : 0u) + (z[j][e] >> p) + 1u + (uint32_t)p : 0u;
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) z[j][e] = 0;
+                }
+            }
+            /* workgroup exclusive scan of tsum */
+            uint32_t v = tsum;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)v, o);
+                if (lane >= o) v += t;
+            }
+            if (lane == 63) red[wid] = v;
+            __syncthreads();
+            uint32_t pre_w = 0, tot = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < NT / 64; ++w2) {
+                const uint32_t s = red[w2];
+                pre_w += w2 < wid ? s : 0u;
+                tot += s;
+            }
+            const uint32_t tstart = tile_base + pre_w + v - tsum;
+            const uint32_t te = tile_base + tot;
+            /* a tile that overruns the ring writes what fits, the full ring leaves, and it
+             * runs again */
+            bool again;
+            do {
+                uint32_t pos = tstart;
+                asm volatile("" : "+v"(pos)); /* opaque: nothing of the body is hoisted out of the redo loop */
+#pragma unroll
+                for (int j = 0; j < MAXC; ++j) {
+                    const int k = k0 + j;
+                    if (k < k1) {
+                        const int i0 = 8 * k;
+                        const int part0 = pt0[j];
+                        if (i0 > order && i0 + 8 <= n && bnd[j] >= i0 + 8) {
+                            const int p = pa[j];
+                            if (i0 == part0 * ps) {
+                                ring_or(pos, (uint32_t)p & pmask_m, (uint32_t)method);
+                                pos += (uint32_t)method;
+                            }
+                            const uint32_t one = 1u << p, wc = (uint32_t)p + 1u;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) {
+                                const uint32_t zk = z[j][e];
+                                const uint32_t P = pos + (zk >> p);
+                                ring_or(P, one | (zk & (one - 1u)), wc);
+                                pos = P + wc;
+                            }
+                        } else { /* the warm-up's chunk, the unit's end, a partition boundary inside */
+#pragma unroll 1
+                            for (int e = 0; e < 8; ++e) {
+                                uint32_t zk = z[j][0];
+#pragma unroll
+                                for (int e2 = 1; e2 < 8; ++e2) zk = e == e2 ? z[j][e2] : zk;
+                                const int i = i0 + e;
+                                if (i >= order && i < n) {
+                                    const int p = i >= bnd[j] ? pb[j] : pa[j];
+                                    if (i == order || i == bnd[j] || i == part0 * ps) {
+                                        ring_or(pos, (uint32_t)p & pmask_m, (uint32_t)method);
+                                        pos += (uint32_t)method;
+                                    }
+                                    const uint32_t P = pos + (zk >> p);
+                                    ring_or(P, (1u << p) | (zk & ((1u << p) - 1u)), (uint32_t)p + 1u); /* p <= 30 */
+                                    pos = P + (uint32_t)p + 1u;
+                                }
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                again = ((te - 1u) >> 5) - fl >= (uint32_t)kWinWords;
+                leave(again ? fl + (uint32_t)kWinWords : te >> 5);
+            } while (again);
+            tile_base = te;
+        }
+    }
+
+    /* CRC-16 of bytes [F, E), E = Fend - 2: the chunks that left (the running CRCs, thread
+     * t's 8-byte words before thread t + 1's in every chunk, joined by a lane tree at
+     * x^(8 * 8 * 2^l) and the waves at x^(8 * 512)), then the ring's words below E (k_pack32's
+     * end fold from word fl), the first shifted past the second */
+    const int64_t E = Fend - 2;
+    {
+        const int nfull = (int)(((E - Fa) >> 2) - (int64_t)fl);
+        int ls = 0;
+        while ((NT << ls) < nfull) ++ls;
+        const int spw = 1 << ls;
+        const int w1 = nfull - (NT - 1 - tid) * spw, w0 = w1 - spw;
+        auto mulx = [&](uint32_t c, int bl) __attribute__((always_inline)) {
+            return (uint32_t)pw[bl * 512 + (c & 0xFF)] ^ (uint32_t)pw[bl * 512 + 256 + (c >> 8)];
+        };
+        uint32_t crc = 0;
+        for (int k = max(w0, 0); k < w1; ++k) crc = crc_fold_word(crc, win[(fl + (uint32_t)k) & kRingMask], ct);
+        uint32_t x = crc_t;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) {
+            const bool right = (lane >> l) & 1;
+            const uint32_t oc = (uint32_t)__shfl_xor((int)crc, 1 << l);
+            crc = mulx(right ? oc : crc, ls + 2 + l) ^ (right ? crc : oc);
+            const uint32_t ox = (uint32_t)__shfl_xor((int)x, 1 << l);
+            x = mulx(right ? ox : x, 3 + l) ^ (right ? x : ox);
+        }
+        if (lane == 0) {
+            red[wid] = crc;
+            red2[wid] = x;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t tcrc = 0, xc = 0;
+            for (int w2 = 0; w2 < NT / 64; ++w2) {
+                tcrc = (w2 ? mulx(tcrc, ls + 8) : 0u) ^ red[w2];
+                xc = (w2 ? mulx(xc, 9) : 0u) ^ red2[w2];
+            }
+            const int tail = (int)(E - Fa - 4 * (int64_t)fl) - 4 * nfull;
+            const uint32_t tw = win[(fl + (uint32_t)nfull) & kRingMask];
+            for (int j = 0; j < tail; ++j) tcrc = ((tcrc << 8) & 0xFFFF) ^ (uint32_t)ct[(tcrc >> 8) ^ ((tw >> (24 - 8 * j)) & 0xFF)];
+            const uint32_t all = crc16_mulpow(xc, E - Fa - 4 * (int64_t)fl, pw) ^ tcrc;
+            ring_or((uint32_t)(8 * (E - Fa)), all & 0xFFFF, 16);
+        }
+        __syncthreads();
+    }
+    /* the ring's last words */
+    const uint32_t endw = (uint32_t)((Fend - Fa + 3) >> 2);
+    for (uint32_t k = fl + 2u * (uint32_t)tid; k < endw; k += 2u * NT) {
+        store8(4u * k, *reinterpret_cast<const uint2*>(&win[k & kRingMask]));
+    }
+}
+
 hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s) {
     if (a.n_frames <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_frame_sizes, dim3((unsigned)((a.n_frames + 3) / 4)), dim3(256), 0, s, a);
@@ -977,14 +1353,37 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     FrameArgs b = a;
-    /* A/B and ablation switches, read once per process (no getenv per launch) */
-    static const bool no_pack32 = getenv("FLACMI_NO_PACK32") != nullptr;
+    /* knob FLACMI_PACK_GENERIC: 1 every frame through k_pack, 2 no k_packw (frames too wide
+     * for k_pack32 go to k_pack), 3 k_packw with 4 chunks a thread a tile (tiles that overrun
+     * the ring: the test of its redo path) */
+    const int pack_generic = knob(kKnobPackGeneric);
+    const bool no_pack32 = pack_generic == 1;
+    const bool no_packw = pack_generic == 1 || pack_generic == 2;
+    /* the ablation switch, read once per process (no getenv per launch) */
     static const int ablate = [] {
         const char* e = getenv("FLACMI_PACK_ABLATE");
         return e ? atoi(e) : 0;
     }();
-    b.pack_split = (tiles == 1 || (nch + nt - 1) / nt <= kMaxC) && !no_pack32;
+    /* k_pack32 / k_packw read residual rows with 16-byte loads */
+    const bool vec_ok = ((uintptr_t)a.residual & 15) == 0 && (a.residual_stride & 3) == 0;
+    const bool wide = !(tiles == 1 || (nch + nt - 1) / nt <= kMaxC);
     b.ablate = ablate;
+    if (wide && vec_ok && !no_pack32 && !no_packw) {
+        /* frames of more than kMaxC chunks a thread: k_packw, 256 threads, 2 chunks a
+         * thread a tile (a tile of 4096 values at <= 28 bits each fits the ring with the
+         * < 512 words still waiting to leave) */
+        b.pack_split = 1;
+        hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
+        if (e0 != hipSuccess) return e0;
+        if (pack_generic == 3) hipLaunchKernelGGL(k_packw<4>, dim3((unsigned)a.n_frames), dim3(kPackThreads), 0, s, b);
+        else hipLaunchKernelGGL(k_packw<2>, dim3((unsigned)a.n_frames), dim3(kPackThreads), 0, s, b);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const int64_t grid = a.n_frames < 4096 ? a.n_frames : 4096;
+        hipLaunchKernelGGL(k_pack<uint32_t>, dim3((unsigned)grid), dim3(nt), 0, s, b);
+        return hipGetLastError();
+    }
+    b.pack_split = !wide && vec_ok && !no_pack32;
     if (b.pack_split) {
         hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
         if (e0 != hipSuccess) return e0;

@@ -78,7 +78,8 @@ def test_knobs_set_get_and_reject_unknown_names():
     environment once; launches never call getenv."""
     from flac_amd.analysis import get_knob, knob
     lib = load()
-    for name in ("FLACMI_OVERLAP", "FLACMI_MF8_GRID", "FLACMI_STREAM_GENERIC", "FLACMI_DECODE_GENERIC"):
+    for name in ("FLACMI_OVERLAP", "FLACMI_MF8_GRID", "FLACMI_STREAM_GENERIC", "FLACMI_DECODE_GENERIC",
+                 "FLACMI_PACK_GENERIC"):
         before = get_knob(name)
         with knob(name, 7):
             assert get_knob(name) == 7

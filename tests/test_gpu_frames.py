@@ -11,6 +11,7 @@ import pytest
 import frame_writer as FW
 import oracle
 from flac_amd import abi
+from flac_amd.analysis import knob
 
 pytestmark = pytest.mark.gpu
 
@@ -118,17 +119,22 @@ def test_device_pointer_path_matches_host_path(az):
     assert not small.cpu().numpy().any()
 
 
-@pytest.mark.parametrize("name", ["c2", "c1_tail", "bs16_3ch"])
-def test_general_writer_alone_matches(az, name, monkeypatch):
-    """FLACMI_NO_PACK32=1: every frame through the general k_pack gives the same bytes."""
+@pytest.mark.parametrize("gen", [1, 2, 3])
+@pytest.mark.parametrize("name", ["c2", "c1_tail", "bs16_3ch", "c3_stereo", "c3_tail", "wide20"])
+def test_general_writer_alone_matches(az, name, gen):
+    """Knob FLACMI_PACK_GENERIC=1 (every frame through the general k_pack) and =2 (k_packw
+    off: frames too wide for k_pack32 go to k_pack) give the default path's bytes; the c3
+    frames exercise k_packw's ring against k_pack, and =3 (k_packw with tiles of 8192
+    values, about 5600 ring words for these 24-bit frames) its redo of a segment that
+    overruns the 4096-word ring."""
     frames, C, n, tail, bits, L, q, rmin, rmax, mode, ss, first, seed = CASES[name]
     rows, n_tail = _rows(frames, C, n, tail, bits, seed)
     params = oracle.make_params(L, q, rmin, rmax, mode)
     want = az.encode_frames(rows, params, n, tail, n_tail, sample_bits=bits, channels=C, sample_size=ss,
                             first_frame=first)
-    monkeypatch.setenv("FLACMI_NO_PACK32", "1")
-    got = az.encode_frames(rows, params, n, tail, n_tail, sample_bits=bits, channels=C, sample_size=ss,
-                           first_frame=first)
+    with knob("FLACMI_PACK_GENERIC", gen):
+        got = az.encode_frames(rows, params, n, tail, n_tail, sample_bits=bits, channels=C, sample_size=ss,
+                               first_frame=first)
     assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2])
     assert got[0].tobytes() == want[0].tobytes()
 

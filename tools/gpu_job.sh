@@ -1,11 +1,11 @@
-# scratch job file for one gpurun call (overwritten per call; the reusable steps are the
-# other tools/gpu_*.sh, pmc_*.sh and profile.sh)
+# scratch GPU job: frame-writer tests, then c3 frame-writer A/B (k_packw vs k_pack)
 set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r6ls; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "frame or decode or writer or cli or encoder" > $O/pt.log 2>&1; rc=$?; tail -1 $O/pt.log; [ $rc -eq 0 ] || { grep -B5 -A30 "FAILED\|Error" $O/pt.log | head -80; exit 1; }
-for spec in c3:5:1 c3:5:0 c3:8:1 c3:0:1 c2:5:1; do
-  c=${spec%%:*}; r=${spec#*:}; k=${r%%:*}; l=${r##*:}
-  FLACMI_DECODE_LPC=$l timeout -k 10 300 python bench.py --config $c --open $k --steps 1 --warmup 1 --cpu-seconds 0 --e2e-units 0 --no-parity > $O/b_${c}_${k}_$l.json 2> $O/err.txt || { tail $O/err.txt; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/b_${c}_${k}_$l.json')); f=d['frame_writer']; r=f['decoder_round_trip']; print('$spec', 'decode', round(r['ms_per_call'],2), r['frames_with_status'], r['samples_mismatched'], 'pack', round(f['ms_per_call'],2))"
+OUT=gpurun_out/packw
+mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_frames.py tests/test_abi.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc $(tail -1 $OUT/pytest.log)"
+[ $rc -eq 0 ] || { grep -B5 -A40 "FAILED\|Error" $OUT/pytest.log | head -80; exit 1; }
+for g in 0 2; do
+  FLACMI_PACK_GENERIC=$g timeout -k 10 300 python bench.py --config c3 --steps 2 --warmup 1 --cpu-seconds 0 --e2e-units 0 > $OUT/c3_g$g.json 2> $OUT/c3_g$g.err || { tail -20 $OUT/c3_g$g.err; exit 1; }
+  python -c "import json;d=json.load(open('$OUT/c3_g$g.json'));f=d['frame_writer'];print('g$g',f['ms_per_call'],f['algorithmic_GBs'],f.get('parity'),f['decoder_round_trip']['samples_mismatched'])"
 done
