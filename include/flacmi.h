@@ -454,7 +454,9 @@ int flacmi_timing_reset(flacmi_ctx* ctx);
  * overlap: -1 round-aligned (default), 0 off, k > 1 equal chunks, -R R units per round),
  * "FLACMI_MF8_GRID" (cap on the int8-MFMA persistent grid, 0 = none), "FLACMI_STREAM_GENERIC"
  * (1 = the runtime-shape stream kernel for 4608-sample units), "FLACMI_DECODE_GENERIC" (1 =
- * every frame of flacmi_decode_frames_device through the general decoder kernel).
+ * every frame of flacmi_decode_frames_device through the general decoder kernel),
+ * "FLACMI_PACK_GENERIC" (frame writer: 1 = every frame through the general writer kernel,
+ * 2 = no ring-window writer for wide frames, 3 = the ring writer with 8192-value tiles).
  * FLACMI_E_INVALID for any other name.  No device needed. */
 int flacmi_set_knob(const char* name, int32_t value);
 int flacmi_get_knob(const char* name, int32_t* value);
