@@ -995,7 +995,7 @@ __device__ __forceinline__ uint32_t crc_fold_word(uint32_t c, uint32_t w, const 
 }
 
 template <int MAXC>
-__global__ __launch_bounds__(kPackThreads) void k_packw(FrameArgs a) {
+__device__ __forceinline__ void packw_frame(const FrameArgs& a) {
     constexpr int NT = kPackThreads; /* the launch uses exactly this many threads */
     __shared__ __align__(16) uint32_t win[kWinWords];
     __shared__ __align__(16) uint16_t ct[4 * 256];
@@ -1241,7 +1241,10 @@ __global__ __launch_bounds__(kPackThreads) void k_packw(FrameArgs a) {
                             const uint32_t one = 1u << p, wc = (uint32_t)p + 1u;
 #pragma unroll
                             for (int e = 0; e < 8; ++e) {
-                                const uint32_t zk = z[j][e];
+                                uint32_t zk = z[j][e];
+                                /* opaque per value: the 8 codes are formed one after the other,
+                                 * not all up front (about 45 fewer VGPRs for 2 chunks) */
+                                asm volatile("" : "+v"(zk));
                                 const uint32_t P = pos + (zk >> p);
                                 ring_or(P, one | (zk & (one - 1u)), wc);
                                 pos = P + wc;
@@ -1326,6 +1329,19 @@ __global__ __launch_bounds__(kPackThreads) void k_packw(FrameArgs a) {
     }
 }
 
+template <int MAXC>
+__global__ __launch_bounds__(kPackThreads) void k_packw(FrameArgs a) {
+    packw_frame<MAXC>(a);
+}
+/* occupancy floors (the kernel is occupancy-bound: 6 waves a SIMD beat 4 and 5): 1 chunk a
+ * thread at 6 waves a SIMD (the default), 2 at 5 (A/B) */
+__global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_packw1_w6(FrameArgs a) {
+    packw_frame<1>(a);
+}
+__global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_packw2_w5(FrameArgs a) {
+    packw_frame<2>(a);
+}
+
 hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s) {
     if (a.n_frames <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_frame_sizes, dim3((unsigned)((a.n_frames + 3) / 4)), dim3(256), 0, s, a);
@@ -1355,7 +1371,9 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     FrameArgs b = a;
     /* knob FLACMI_PACK_GENERIC: 1 every frame through k_pack, 2 no k_packw (frames too wide
      * for k_pack32 go to k_pack), 3 k_packw with 4 chunks a thread a tile (tiles that overrun
-     * the ring: the test of its redo path) */
+     * the ring: the test of its redo path), 4-6 k_packw A/B builds (2 chunks a thread, 113
+     * VGPRs; 1 chunk, 88; 2 chunks held to 5 waves a SIMD).  Default: 1 chunk a thread held
+     * to 6 waves a SIMD (79 VGPRs, no spills): c3 frames 6.29 / 5.84 / 5.86 -> 5.40 ms */
     const int pack_generic = knob(kKnobPackGeneric);
     const bool no_pack32 = pack_generic == 1;
     const bool no_packw = pack_generic == 1 || pack_generic == 2;
@@ -1369,14 +1387,19 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     const bool wide = !(tiles == 1 || (nch + nt - 1) / nt <= kMaxC);
     b.ablate = ablate;
     if (wide && vec_ok && !no_pack32 && !no_packw) {
-        /* frames of more than kMaxC chunks a thread: k_packw, 256 threads, 2 chunks a
-         * thread a tile (a tile of 4096 values at <= 28 bits each fits the ring with the
-         * < 512 words still waiting to leave) */
+        /* frames of more than kMaxC chunks a thread: k_packw, 256 threads, 1 chunk a thread
+         * a tile (a tile of 2048 values fits the ring above the < 512 words still waiting
+         * to leave up to 56 bits a value on average; a longer one, e.g. long unary runs of
+         * outliers, takes the redo path) */
         b.pack_split = 1;
         hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
         if (e0 != hipSuccess) return e0;
-        if (pack_generic == 3) hipLaunchKernelGGL(k_packw<4>, dim3((unsigned)a.n_frames), dim3(kPackThreads), 0, s, b);
-        else hipLaunchKernelGGL(k_packw<2>, dim3((unsigned)a.n_frames), dim3(kPackThreads), 0, s, b);
+        const dim3 g((unsigned)a.n_frames), t(kPackThreads);
+        if (pack_generic == 3) hipLaunchKernelGGL(k_packw<4>, g, t, 0, s, b);
+        else if (pack_generic == 4) hipLaunchKernelGGL(k_packw<2>, g, t, 0, s, b);
+        else if (pack_generic == 5) hipLaunchKernelGGL(k_packw<1>, g, t, 0, s, b);
+        else if (pack_generic == 6) hipLaunchKernelGGL(k_packw2_w5, g, t, 0, s, b);
+        else hipLaunchKernelGGL(k_packw1_w6, g, t, 0, s, b);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         const int64_t grid = a.n_frames < 4096 ? a.n_frames : 4096;
