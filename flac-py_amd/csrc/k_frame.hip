@@ -36,6 +36,7 @@
 namespace flacmi {
 
 constexpr int kWinWords = 4096;           /* 16 KB LDS window */
+constexpr int kWinSmall = 3072;           /* k_pack32's window for frames of <= ~9.8 KB */
 constexpr int kPackThreads = 256;
 constexpr int kCrcPowLevels = 28;         /* frames < 2^28 bytes */
 
@@ -320,9 +321,9 @@ __device__ void win_flush(const FrameArgs& a, uint32_t* win, const uint16_t* ct,
  * partition boundary); the launch guarantees 32-bit residuals and <= kMaxC chunks per
  * thread. */
 constexpr int kMaxC = 4;
-__device__ __forceinline__ bool pack32_frame_ok(const FrameArgs& a, int64_t f) {
+__device__ __forceinline__ bool pack32_frame_ok(const FrameArgs& a, int64_t f, int ww) {
     const int64_t bytes = a.offsets[f + 1] - a.offsets[f];
-    if (bytes + 8 > 4LL * kWinWords) return false;
+    if (bytes + 8 > 4LL * ww) return false;
     for (int c = 0; c < a.channels; ++c) {
         const int64_t u = f * a.channels + c;
         if ((unit_len(a, u) >> a.meta[u].part_order) < 8) return false;
@@ -637,10 +638,14 @@ __device__ __forceinline__ void or_bits(uint32_t* win, uint32_t P, uint32_t val,
     atomicOr(wp + 1, (uint32_t)t);
 }
 
-template <int MAXC> /* chunks per thread the launch guarantees (2..kMaxC): fewer registers, more
-                     * frames in flight per CU */
-__global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
-    __shared__ uint32_t win[kWinWords];
+/* MAXC: chunks per thread the launch guarantees (2..kMaxC): fewer registers, more frames in
+ * flight per CU.  WW: window words (frames larger go to k_pack by list); WPE: occupancy floor
+ * in waves a SIMD.  A 3072-word window (14.3 KB of LDS) lets 10 workgroups share a CU, so
+ * the floor of 7 waves (72 VGPRs, no spills) is reachable; the 16 KB window capped it at 8
+ * workgroups, 6 waves a SIMD for 192-thread groups. */
+template <int MAXC, int WW, int WPE>
+__global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_pack32(FrameArgs a) {
+    __shared__ uint32_t win[WW];
     __shared__ __align__(16) uint16_t ct[4 * 256];
     __shared__ uint8_t hdr[16];
     __shared__ uint32_t sub_start[9];
@@ -662,7 +667,7 @@ __global__ __launch_bounds__(kPackThreads) void k_pack32(FrameArgs a) {
     }
     if (a.offsets[a.n_frames] > a.capacity) return; /* k_pack reports it */
     if (a.status[f] != 0) return;
-    if (!pack32_frame_ok(a, f)) { /* k_pack writes it */
+    if (!pack32_frame_ok(a, f, WW)) { /* k_pack writes it */
         if (threadIdx.x == 0) a.slow_list[atomicAdd(a.slow_count, 1ull)] = f;
         return;
     }
@@ -1333,13 +1338,10 @@ template <int MAXC>
 __global__ __launch_bounds__(kPackThreads) void k_packw(FrameArgs a) {
     packw_frame<MAXC>(a);
 }
-/* occupancy floors (the kernel is occupancy-bound: 6 waves a SIMD beat 4 and 5): 1 chunk a
- * thread at 6 waves a SIMD (the default), 2 at 5 (A/B) */
+/* the default build: 1 chunk a thread held to 6 waves a SIMD (the kernel is occupancy-bound:
+ * 6 waves a SIMD beat 4 and 5; 2 chunks held to 5 spilled and lost) */
 __global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_packw1_w6(FrameArgs a) {
     packw_frame<1>(a);
-}
-__global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_packw2_w5(FrameArgs a) {
-    packw_frame<2>(a);
 }
 
 hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s) {
@@ -1371,9 +1373,9 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     FrameArgs b = a;
     /* knob FLACMI_PACK_GENERIC: 1 every frame through k_pack, 2 no k_packw (frames too wide
      * for k_pack32 go to k_pack), 3 k_packw with 4 chunks a thread a tile (tiles that overrun
-     * the ring: the test of its redo path), 4-6 k_packw A/B builds (2 chunks a thread, 113
-     * VGPRs; 1 chunk, 88; 2 chunks held to 5 waves a SIMD).  Default: 1 chunk a thread held
-     * to 6 waves a SIMD (79 VGPRs, no spills): c3 frames 6.29 / 5.84 / 5.86 -> 5.40 ms */
+     * the ring: the test of its redo path), 4-5 k_packw A/B builds (2 chunks a thread, 113
+     * VGPRs; 1 chunk, 88).  Default: 1 chunk a thread held to 6 waves a SIMD (79 VGPRs, no
+     * spills): c3 frames 6.29 / 5.84 -> 5.40 ms.  7: k_pack32 with the 16 KB window only */
     const int pack_generic = knob(kKnobPackGeneric);
     const bool no_pack32 = pack_generic == 1;
     const bool no_packw = pack_generic == 1 || pack_generic == 2;
@@ -1398,7 +1400,6 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
         if (pack_generic == 3) hipLaunchKernelGGL(k_packw<4>, g, t, 0, s, b);
         else if (pack_generic == 4) hipLaunchKernelGGL(k_packw<2>, g, t, 0, s, b);
         else if (pack_generic == 5) hipLaunchKernelGGL(k_packw<1>, g, t, 0, s, b);
-        else if (pack_generic == 6) hipLaunchKernelGGL(k_packw2_w5, g, t, 0, s, b);
         else hipLaunchKernelGGL(k_packw1_w6, g, t, 0, s, b);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -1411,9 +1412,20 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
         hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
         if (e0 != hipSuccess) return e0;
         const int cpt = (nch + nt - 1) / nt;
-        if (cpt <= 2) hipLaunchKernelGGL(k_pack32<2>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
-        else if (cpt == 3) hipLaunchKernelGGL(k_pack32<3>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
-        else hipLaunchKernelGGL(k_pack32<kMaxC>, dim3((unsigned)a.n_frames), dim3(nt), 0, s, b);
+        const dim3 g((unsigned)a.n_frames), t(nt);
+        /* the small window when a verbatim frame fits it with room (Rice frames larger than
+         * that go to k_pack) */
+        const int64_t verb = (int64_t)a.block_len * a.sample_size * a.channels / 8 + 64;
+        const bool small = verb + verb / 4 <= 4LL * kWinSmall && pack_generic != 7;
+        if (small) {
+            if (cpt <= 2) hipLaunchKernelGGL((k_pack32<2, kWinSmall, 7>), g, t, 0, s, b);
+            else if (cpt == 3) hipLaunchKernelGGL((k_pack32<3, kWinSmall, 7>), g, t, 0, s, b);
+            else hipLaunchKernelGGL((k_pack32<kMaxC, kWinSmall, 5>), g, t, 0, s, b);
+        } else {
+            if (cpt <= 2) hipLaunchKernelGGL((k_pack32<2, kWinWords, 1>), g, t, 0, s, b);
+            else if (cpt == 3) hipLaunchKernelGGL((k_pack32<3, kWinWords, 1>), g, t, 0, s, b);
+            else hipLaunchKernelGGL((k_pack32<kMaxC, kWinWords, 1>), g, t, 0, s, b);
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
