@@ -25,6 +25,12 @@
  *                  contiguous run of window words with slice-by-4 tables and moves the
  *                  partial CRC to the frame's end with x^(8d) tables (the CRC is linear
  *                  and starts from 0, so CRC(A||B) = CRC(A)*x^(8|B|) + CRC(B) mod P).
+ *                  The general writer: 64-bit residuals, partitions under 8 values and
+ *                  the frames the two kernels below hand over by list.
+ *   k_pack32       frames that fit one LDS window (12 KB when a verbatim frame fits it,
+ *                  else 16 KB): contiguous chunk runs per thread, one scan per subframe.
+ *   k_packw        frames wider than k_pack32 takes (config 3): the window as a ring,
+ *                  finished 2 KB chunks leaving it as the tiles advance.
  *
  * Bit coordinates inside k_pack are "aligned": bit 0 is the MSB of the 32-bit word that
  * holds the frame's first byte, so window word k is output word (F >> 2) + wb + k.  The
