@@ -38,6 +38,12 @@ CASES = {
     "wide20": (6, 2, 4096, 0, 20, 12, 14, 0, 6, 0, 20, 9, 20),
     # frames > the 16 KB LDS window while k_pack32 is active: handed to k_pack by list
     "big3ch_list": (8, 3, 4608, 0, 20, 12, 12, 0, 5, 0, 20, 3, 21),
+    # k_packw batches: a block that is not a multiple of 8 (the row's last chunk read value by
+    # value), 5-value partitions (order 11 at 10240: every frame handed to k_pack by list), and
+    # 16-bit stereo 16384-sample frames with a short last frame
+    "wide_odd": (3, 2, 9001, 0, 16, 8, 12, 0, 4, 0, 16, 5, 22),
+    "wide_fine": (3, 1, 10240, 0, 16, 0, 5, 11, 11, 1, 16, 7, 23),
+    "wide16_tail": (3, 2, 16384, 5000, 16, 12, 12, 0, 8, 0, 16, 9, 24),
 }
 
 
@@ -120,7 +126,8 @@ def test_device_pointer_path_matches_host_path(az):
 
 
 @pytest.mark.parametrize("gen", [1, 2, 3, 7])
-@pytest.mark.parametrize("name", ["c2", "c1_tail", "bs16_3ch", "c3_stereo", "c3_tail", "wide20"])
+@pytest.mark.parametrize("name", ["c2", "c1_tail", "bs16_3ch", "c3_stereo", "c3_tail", "wide20", "wide_odd",
+                                  "wide_fine", "wide16_tail"])
 def test_general_writer_alone_matches(az, name, gen):
     """Knob FLACMI_PACK_GENERIC=1 (every frame through the general k_pack) and =2 (k_packw
     off: frames too wide for k_pack32 go to k_pack) give the default path's bytes; the c3
@@ -141,7 +148,8 @@ def test_general_writer_alone_matches(az, name, gen):
 
 
 @pytest.mark.parametrize("name,upb", [("c2", 5), ("c1_tail", 4), ("c3_stereo", 2), ("bs16_3ch", 3),
-                                      ("q16_assert", 12), ("wide20", 4), ("big3ch_list", 6)])
+                                      ("q16_assert", 12), ("wide20", 4), ("big3ch_list", 6),
+                                      ("wide_odd", 2), ("wide16_tail", 2)])
 def test_encode_pipeline_equals_encode_frames(az, name, upb):
     """flacmi_encode_pipeline (sub-batches of upb frames, three in flight, the caller's
     buffers page-locked in place) gives the bytes, offsets and statuses of the one-shot
