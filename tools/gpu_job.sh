@@ -1,8 +1,9 @@
-# scratch GPU job: c2 frame-writer A/B (k_pack32 small window at 7 vs 8 waves a SIMD)
+# scratch GPU job: the whole GPU suite and smoke on the committed tree
 set -o pipefail
-OUT=gpurun_out/pack32b
+OUT=gpurun_out/final_suite
 mkdir -p $OUT
-for g in 0 8 0 8; do
-  FLACMI_PACK_GENERIC=$g timeout -k 10 300 python bench.py --steps 2 --warmup 1 --cpu-seconds 0 --e2e-units 0 > $OUT/c2_g$g.json 2> $OUT/c2_g$g.err || { tail -20 $OUT/c2_g$g.err; exit 1; }
-  python -c "import json;d=json.load(open('$OUT/c2_g$g.json'));f=d['frame_writer'];print('g$g',f['ms_per_call'],f['algorithmic_GBs'],f.get('parity'),f['decoder_round_trip']['samples_mismatched'])"
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc $(tail -1 $OUT/pytest_gpu.log)"
+[ $rc -eq 0 ] || { grep -B5 -A30 "FAILED\|Error" $OUT/pytest_gpu.log | head -60; exit 1; }
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
