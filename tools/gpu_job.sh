@@ -1,9 +1,8 @@
-# scratch GPU job: the whole GPU suite and smoke on the committed tree
+# scratch GPU job: c3 frame-writer A/B (k_packw 256 threads vs 512 threads on a 32 / 16 KB ring)
 set -o pipefail
-OUT=gpurun_out/final_suite
+OUT=gpurun_out/packw512
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc $(tail -1 $OUT/pytest_gpu.log)"
-[ $rc -eq 0 ] || { grep -B5 -A30 "FAILED\|Error" $OUT/pytest_gpu.log | head -60; exit 1; }
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
-tail -1 $OUT/smoke.log
+for g in 0 6 8 0 6 8; do
+  FLACMI_PACK_GENERIC=$g timeout -k 10 300 python bench.py --config c3 --steps 2 --warmup 1 --cpu-seconds 0 --e2e-units 0 > $OUT/c3_g$g.json 2> $OUT/c3_g$g.err || { tail -20 $OUT/c3_g$g.err; exit 1; }
+  python -c "import json;d=json.load(open('$OUT/c3_g$g.json'));f=d['frame_writer'];print('g$g',f['ms_per_call'],f['algorithmic_GBs'],f.get('parity'),f['decoder_round_trip']['samples_mismatched'],f['decoder_round_trip']['frames_with_status'])"
+done
