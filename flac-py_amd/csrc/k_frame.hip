@@ -973,24 +973,22 @@ __global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(WP
  *
  * k_pack32's placement run tile after tile: a tile is NT * MAXC chunks, one workgroup scan
  * gives each thread the bit position of its contiguous run, and every code is ORed into
- * LDS at its bit position.  The LDS window is a ring of kWinWords words; window bit 0 is
- * the 16-byte aligned output address at or below the frame's first byte.  Bits below a
+ * LDS at its bit position.  The LDS window is a ring of RW words; window bit 0 is the
+ * 16-byte aligned output address at or below the frame's first byte.  Bits below a
  * segment's end (the frame header, a subframe's header fields, a tile) are final, so after
- * each segment the whole kRingChunk-word chunks below it leave the ring: thread t takes
- * words 2t and 2t+1 of the chunk (one 8-byte LDS read, one 8-byte store, zeroed behind),
- * folds their CRC-16 and adds it to its own running CRC multiplied by x^(8 * 2048) (the
- * chunk length; one table in LDS).  At the frame's end a lane tree turns the 256 running
- * CRCs into the CRC of everything that left, k_pack32's end fold takes the last < 512
- * words, and the two are joined with one x^(8d) multiplication.  A segment that would
- * overrun the ring writes what fits (ORs outside [fl, fl + kWinWords) are skipped), the
- * full ring leaves, and the segment runs again: ORs are idempotent.  The general k_pack
- * flushes a whole window at a time with a per-thread x^(8d) shift from global tables (17
- * dependent loads a flush) and one-value-at-a-time accumulators; this kernel is its
- * replacement for the frames it takes (the rest go to k_pack by list).
+ * each segment the whole 2 NT-word chunks below it leave the ring: thread t takes words 2t
+ * and 2t+1 of the chunk (one 8-byte LDS read, one 8-byte store, zeroed behind), folds their
+ * CRC-16 and adds it to its own running CRC multiplied by x^(8 * 8 NT) (the chunk length;
+ * one table in LDS).  At the frame's end a lane tree turns the running CRCs into the CRC
+ * of everything that left, k_pack32's end fold takes the last < 2 NT words, and the two
+ * are joined with one x^(8d) multiplication.  A segment that would overrun the ring writes
+ * what fits (ORs outside [fl, fl + RW) are skipped), the full ring leaves, and the segment
+ * runs again: ORs are idempotent.  The default build is one wave a workgroup (NT = 64, a
+ * 4 KB ring), so its barriers are one wave's.  The general k_pack flushes a whole window at
+ * a time with a per-thread x^(8d) shift from global tables (17 dependent loads a flush) and
+ * one-value-at-a-time accumulators; this kernel is its replacement for the frames it takes
+ * (the rest go to k_pack by list).
  * ==================================================================================== */
-constexpr uint32_t kRingMask = kWinWords - 1;
-constexpr int kRingChunk = 2 * kPackThreads; /* words leaving the ring together: 2048 bytes */
-constexpr int kRingChunkLevel = 11;          /* x^(8 * 2^11) */
 
 __device__ __forceinline__ bool packw_frame_ok(const FrameArgs& a, int64_t f) {
     for (int c = 0; c < a.channels; ++c) {
@@ -1005,12 +1003,15 @@ __device__ __forceinline__ uint32_t crc_fold_word(uint32_t c, uint32_t w, const 
            (uint32_t)ct[256 + ((w >> 8) & 0xFF)] ^ (uint32_t)ct[w & 0xFF];
 }
 
-template <int MAXC>
+template <int MAXC, int NT, int RW> /* NT: the launch's threads; RW: ring words */
 __device__ __forceinline__ void packw_frame(const FrameArgs& a) {
-    constexpr int NT = kPackThreads; /* the launch uses exactly this many threads */
-    __shared__ __align__(16) uint32_t win[kWinWords];
+    constexpr uint32_t RM = RW - 1;
+    constexpr int CH = 2 * NT;                    /* words leaving the ring together */
+    constexpr int CHL = NT == 64 ? 9 : NT == 128 ? 10 : 11; /* x^(8 * 4 CH) = x^(8 * 2^CHL) */
+    static_assert(NT == 64 || NT == 128 || NT == 256, "k_packw runs 64, 128 or 256 threads");
+    __shared__ __align__(16) uint32_t win[RW];
     __shared__ __align__(16) uint16_t ct[4 * 256];
-    __shared__ __align__(16) uint16_t pwc[512]; /* c -> c * x^(8 * kRingChunk * 4) */
+    __shared__ __align__(16) uint16_t pwc[512]; /* c -> c * x^(8 * CH * 4) */
     __shared__ uint8_t hdr[16];
     __shared__ uint32_t sub_start[9];
     __shared__ int32_t cnt14[8];
@@ -1034,8 +1035,8 @@ __device__ __forceinline__ void packw_frame(const FrameArgs& a) {
     const uint16_t* __restrict__ pw = a.crc_pow;
     for (int i = tid; i < 128; i += NT) reinterpret_cast<uint4*>(ct)[i] = reinterpret_cast<const uint4*>(a.crc_slice)[i];
     for (int i = tid; i < 64; i += NT)
-        reinterpret_cast<uint4*>(pwc)[i] = reinterpret_cast<const uint4*>(pw + kRingChunkLevel * 512)[i];
-    for (int i = tid; i < kWinWords / 4; i += NT) reinterpret_cast<uint4*>(win)[i] = uint4{0, 0, 0, 0};
+        reinterpret_cast<uint4*>(pwc)[i] = reinterpret_cast<const uint4*>(pw + CHL * 512)[i];
+    for (int i = tid; i < RW / 4; i += NT) reinterpret_cast<uint4*>(win)[i] = uint4{0, 0, 0, 0};
     if (tid < 8) cnt14[tid] = 0;
     if (tid == 0) hb_s = frame_header(a.first_frame + f, unit_len(a, u0), hdr);
     __syncthreads();
@@ -1068,8 +1069,8 @@ __device__ __forceinline__ void packw_frame(const FrameArgs& a) {
     auto ring_or = [&](uint32_t P, uint32_t val, uint32_t w) __attribute__((always_inline)) {
         const uint64_t t = (uint64_t)val << (64u - (P & 31u) - w);
         const uint32_t wi = P >> 5;
-        if (wi - fl < (uint32_t)kWinWords) atomicOr(&win[wi & kRingMask], (uint32_t)(t >> 32));
-        if (wi + 1u - fl < (uint32_t)kWinWords) atomicOr(&win[(wi + 1u) & kRingMask], (uint32_t)t);
+        if (wi - fl < (uint32_t)RW) atomicOr(&win[wi & RM], (uint32_t)(t >> 32));
+        if (wi + 1u - fl < (uint32_t)RW) atomicOr(&win[(wi + 1u) & RM], (uint32_t)t);
     };
     /* whole chunks below ring word upto leave: CRC share, store, zero; frame bytes are
      * [fb0, fb1) in window bytes */
@@ -1087,22 +1088,22 @@ __device__ __forceinline__ void packw_frame(const FrameArgs& a) {
         }
     };
     auto leave = [&](uint32_t upto) __attribute__((always_inline)) {
-        if (upto - fl < (uint32_t)kRingChunk) return;
+        if (upto - fl < (uint32_t)CH) return;
         do {
             const uint32_t k = fl + 2u * (uint32_t)tid;
-            uint2* wp = reinterpret_cast<uint2*>(&win[k & kRingMask]);
+            uint2* wp = reinterpret_cast<uint2*>(&win[k & RM]);
             const uint2 w = *wp;
             *wp = uint2{0, 0};
             const uint32_t c = crc_fold_word(crc_fold_word(0, w.x, ct), w.y, ct);
             crc_t = ((uint32_t)pwc[crc_t & 0xFF] ^ (uint32_t)pwc[256 + (crc_t >> 8)]) ^ c;
             store8(4u * k, w);
-            fl += (uint32_t)kRingChunk;
-        } while (upto - fl >= (uint32_t)kRingChunk);
+            fl += (uint32_t)CH;
+        } while (upto - fl >= (uint32_t)CH);
         __syncthreads(); /* zeroed words are written again by the next segment */
     };
 
     /* the frame header and a subframe's header fields (< 1600 bits) always fit the ring
-     * above the < kRingChunk words still waiting */
+     * above the < CH words still waiting */
     if (tid < hb) ring_or(A + 8u * tid, hdr[tid], 8);
     __syncthreads();
     leave((A + 8u * hb) >> 5);
@@ -1282,8 +1283,8 @@ __device__ __forceinline__ void packw_frame(const FrameArgs& a) {
                     }
                 }
                 __syncthreads();
-                again = ((te - 1u) >> 5) - fl >= (uint32_t)kWinWords;
-                leave(again ? fl + (uint32_t)kWinWords : te >> 5);
+                again = ((te - 1u) >> 5) - fl >= (uint32_t)RW;
+                leave(again ? fl + (uint32_t)RW : te >> 5);
             } while (again);
             tile_base = te;
         }
@@ -1304,7 +1305,7 @@ __device__ __forceinline__ void packw_frame(const FrameArgs& a) {
             return (uint32_t)pw[bl * 512 + (c & 0xFF)] ^ (uint32_t)pw[bl * 512 + 256 + (c >> 8)];
         };
         uint32_t crc = 0;
-        for (int k = max(w0, 0); k < w1; ++k) crc = crc_fold_word(crc, win[(fl + (uint32_t)k) & kRingMask], ct);
+        for (int k = max(w0, 0); k < w1; ++k) crc = crc_fold_word(crc, win[(fl + (uint32_t)k) & RM], ct);
         uint32_t x = crc_t;
 #pragma unroll
         for (int l = 0; l < 6; ++l) {
@@ -1326,7 +1327,7 @@ __device__ __forceinline__ void packw_frame(const FrameArgs& a) {
                 xc = (w2 ? mulx(xc, 9) : 0u) ^ red2[w2];
             }
             const int tail = (int)(E - Fa - 4 * (int64_t)fl) - 4 * nfull;
-            const uint32_t tw = win[(fl + (uint32_t)nfull) & kRingMask];
+            const uint32_t tw = win[(fl + (uint32_t)nfull) & RM];
             for (int j = 0; j < tail; ++j) tcrc = ((tcrc << 8) & 0xFFFF) ^ (uint32_t)ct[(tcrc >> 8) ^ ((tw >> (24 - 8 * j)) & 0xFF)];
             const uint32_t all = crc16_mulpow(xc, E - Fa - 4 * (int64_t)fl, pw) ^ tcrc;
             ring_or((uint32_t)(8 * (E - Fa)), all & 0xFFFF, 16);
@@ -1336,18 +1337,27 @@ __device__ __forceinline__ void packw_frame(const FrameArgs& a) {
     /* the ring's last words */
     const uint32_t endw = (uint32_t)((Fend - Fa + 3) >> 2);
     for (uint32_t k = fl + 2u * (uint32_t)tid; k < endw; k += 2u * NT) {
-        store8(4u * k, *reinterpret_cast<const uint2*>(&win[k & kRingMask]));
+        store8(4u * k, *reinterpret_cast<const uint2*>(&win[k & RM]));
     }
 }
 
-template <int MAXC>
-__global__ __launch_bounds__(kPackThreads) void k_packw(FrameArgs a) {
-    packw_frame<MAXC>(a);
+/* the default build: 64 threads (one wave: the workgroup's barriers are one wave's), a 4 KB
+ * ring, one chunk a thread, held to 6 waves a SIMD (76 VGPRs, no spills).  c3 frames, same
+ * box: 256 threads on a 16 KB ring 5.53-5.56 ms, 128 threads on 8 KB 5.13-5.14, 64 on 4 KB
+ * 5.08.  k_packw_redo_test's MAXC = 4 (knob 3) gives 2048-value tiles, about 1400 ring words for 24-bit frames,
+ * for the tests of the redo of a tile that overruns the ring. */
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_packw(FrameArgs a) {
+    packw_frame<1, 64, 1024>(a);
 }
-/* the default build: 1 chunk a thread held to 6 waves a SIMD (the kernel is occupancy-bound:
- * 6 waves a SIMD beat 4 and 5; 2 chunks held to 5 spilled and lost) */
-__global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_packw1_w6(FrameArgs a) {
-    packw_frame<1>(a);
+__global__ __launch_bounds__(64) void k_packw_redo_test(FrameArgs a) { /* knob 3 (no occupancy floor) */
+    packw_frame<4, 64, 1024>(a);
+}
+/* A/B builds: 256 threads on a 16 KB ring (the first default), 128 threads on an 8 KB ring */
+__global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_packw256(FrameArgs a) {
+    packw_frame<1, kPackThreads, kWinWords>(a);
+}
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_packw128(FrameArgs a) {
+    packw_frame<1, 128, 2048>(a);
 }
 
 hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s) {
@@ -1378,10 +1388,9 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     }
     FrameArgs b = a;
     /* knob FLACMI_PACK_GENERIC: 1 every frame through k_pack, 2 no k_packw (frames too wide
-     * for k_pack32 go to k_pack), 3 k_packw with 4 chunks a thread a tile (tiles that overrun
-     * the ring: the test of its redo path), 4-5 k_packw A/B builds (2 chunks a thread, 113
-     * VGPRs; 1 chunk, 88).  Default: 1 chunk a thread held to 6 waves a SIMD (79 VGPRs, no
-     * spills): c3 frames 6.29 / 5.84 -> 5.40 ms.  7: k_pack32 with the 16 KB window only */
+     * for k_pack32 go to k_pack), 3 k_packw with 2048-value tiles (tiles that overrun the ring:
+     * the test of its redo path), 6 / 8 k_packw A/B builds (256 / 128 threads), 7 k_pack32 on
+     * its 16 KB window only */
     const int pack_generic = knob(kKnobPackGeneric);
     const bool no_pack32 = pack_generic == 1;
     const bool no_packw = pack_generic == 1 || pack_generic == 2;
@@ -1395,18 +1404,18 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     const bool wide = !(tiles == 1 || (nch + nt - 1) / nt <= kMaxC);
     b.ablate = ablate;
     if (wide && vec_ok && !no_pack32 && !no_packw) {
-        /* frames of more than kMaxC chunks a thread: k_packw, 256 threads, 1 chunk a thread
-         * a tile (a tile of 2048 values fits the ring above the < 512 words still waiting
-         * to leave up to 56 bits a value on average; a longer one, e.g. long unary runs of
+        /* frames of more than kMaxC chunks a thread: k_packw, 64 threads, 1 chunk a thread a
+         * tile (a tile of 512 values fits the ring above the < 128 words still waiting to
+         * leave up to 56 bits a value on average; a longer one, e.g. long unary runs of
          * outliers, takes the redo path) */
         b.pack_split = 1;
         hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
         if (e0 != hipSuccess) return e0;
-        const dim3 g((unsigned)a.n_frames), t(kPackThreads);
-        if (pack_generic == 3) hipLaunchKernelGGL(k_packw<4>, g, t, 0, s, b);
-        else if (pack_generic == 4) hipLaunchKernelGGL(k_packw<2>, g, t, 0, s, b);
-        else if (pack_generic == 5) hipLaunchKernelGGL(k_packw<1>, g, t, 0, s, b);
-        else hipLaunchKernelGGL(k_packw1_w6, g, t, 0, s, b);
+        const dim3 g((unsigned)a.n_frames);
+        if (pack_generic == 3) hipLaunchKernelGGL(k_packw_redo_test, g, dim3(64), 0, s, b);
+        else if (pack_generic == 6) hipLaunchKernelGGL(k_packw256, g, dim3(kPackThreads), 0, s, b);
+        else if (pack_generic == 8) hipLaunchKernelGGL(k_packw128, g, dim3(128), 0, s, b);
+        else hipLaunchKernelGGL(k_packw, g, dim3(64), 0, s, b);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         const int64_t grid = a.n_frames < 4096 ? a.n_frames : 4096;

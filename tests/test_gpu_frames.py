@@ -131,9 +131,9 @@ def test_device_pointer_path_matches_host_path(az):
 def test_general_writer_alone_matches(az, name, gen):
     """Knob FLACMI_PACK_GENERIC=1 (every frame through the general k_pack) and =2 (k_packw
     off: frames too wide for k_pack32 go to k_pack) give the default path's bytes; the c3
-    frames exercise k_packw's ring against k_pack, and =3 (k_packw with tiles of 8192
-    values, about 5600 ring words for these 24-bit frames) its redo of a segment that
-    overruns the 4096-word ring; =7 keeps k_pack32 on its 16 KB window (the default takes
+    frames exercise k_packw's ring against k_pack, and =3 (k_packw with tiles of 2048
+    values, about 1400 ring words for these 24-bit frames) its redo of a segment that
+    overruns the 1024-word ring; =7 keeps k_pack32 on its 16 KB window (the default takes
     the 12 KB window when a verbatim frame fits it with a quarter to spare)."""
     frames, C, n, tail, bits, L, q, rmin, rmax, mode, ss, first, seed = CASES[name]
     rows, n_tail = _rows(frames, C, n, tail, bits, seed)
