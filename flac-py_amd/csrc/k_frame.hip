@@ -1387,13 +1387,16 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     FrameArgs b = a;
-    /* knob FLACMI_PACK_GENERIC: 1 every frame through k_pack, 2 no k_packw (frames too wide
-     * for k_pack32 go to k_pack), 3 k_packw with 2048-value tiles (tiles that overrun the ring:
-     * the test of its redo path), 6 / 8 k_packw A/B builds (256 / 128 threads), 7 k_pack32 on
-     * its 16 KB window only */
+    /* knob FLACMI_PACK_GENERIC: 1 every frame through k_pack; 2 no k_packw (k_pack32 for the
+     * frames it fits, k_pack for the rest: the writer before k_packw); 3 k_packw with
+     * 2048-value tiles (tiles that overrun the ring: the test of its redo path); 6 / 8 k_packw
+     * built for 256 / 128 threads (A/B); 7 as 2 with k_pack32 on its 16 KB window only.
+     * Default: k_packw for every batch of 32-bit residual rows it can read with 16-byte loads
+     * (one wave a frame beat k_pack32's one workgroup a frame on config 2 too: 8.02 against
+     * 8.48-8.49 ms per 1e6 frames, same box) */
     const int pack_generic = knob(kKnobPackGeneric);
     const bool no_pack32 = pack_generic == 1;
-    const bool no_packw = pack_generic == 1 || pack_generic == 2;
+    const bool no_packw = pack_generic == 1 || pack_generic == 2 || pack_generic == 7;
     /* the ablation switch, read once per process (no getenv per launch) */
     static const int ablate = [] {
         const char* e = getenv("FLACMI_PACK_ABLATE");
@@ -1403,11 +1406,10 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
     const bool vec_ok = ((uintptr_t)a.residual & 15) == 0 && (a.residual_stride & 3) == 0;
     const bool wide = !(tiles == 1 || (nch + nt - 1) / nt <= kMaxC);
     b.ablate = ablate;
-    if (wide && vec_ok && !no_pack32 && !no_packw) {
-        /* frames of more than kMaxC chunks a thread: k_packw, 64 threads, 1 chunk a thread a
-         * tile (a tile of 512 values fits the ring above the < 128 words still waiting to
-         * leave up to 56 bits a value on average; a longer one, e.g. long unary runs of
-         * outliers, takes the redo path) */
+    if (vec_ok && !no_packw) {
+        /* k_packw, 64 threads, 1 chunk a thread a tile (a tile of 512 values fits the ring
+         * above the < 128 words still waiting to leave up to 56 bits a value on average; a
+         * longer one, e.g. long unary runs of outliers, takes the redo path) */
         b.pack_split = 1;
         hipError_t e0 = hipMemsetAsync(b.slow_count, 0, sizeof(unsigned long long), s);
         if (e0 != hipSuccess) return e0;

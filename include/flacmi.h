@@ -456,9 +456,9 @@ int flacmi_timing_reset(flacmi_ctx* ctx);
  * (1 = the runtime-shape stream kernel for 4608-sample units), "FLACMI_DECODE_GENERIC" (1 =
  * every frame of flacmi_decode_frames_device through the general decoder kernel),
  * "FLACMI_PACK_GENERIC" (frame writer: 1 = every frame through the general writer kernel,
- * 2 = no ring-window writer for wide frames, 3 = the ring writer with 2048-value tiles,
- * 6 / 8 = the ring writer built for 256 / 128 threads, 7 = the small-frame writer on its
- * 16 KB window only).
+ * 2 = no ring-window writer (the one-window writer where a frame fits, else the general one),
+ * 3 = the ring writer with 2048-value tiles, 6 / 8 = the ring writer built for 256 / 128
+ * threads, 7 = as 2 with the one-window writer on its 16 KB window only).
  * FLACMI_E_INVALID for any other name.  No device needed. */
 int flacmi_set_knob(const char* name, int32_t value);
 int flacmi_get_knob(const char* name, int32_t* value);

@@ -36,7 +36,8 @@ CASES = {
     "q16_assert": (12, 1, 1152, 0, 16, 8, 16, 0, 4, 0, 16, 0, 18),
     "overflow": (6, 1, 576, 0, 16, 4, 5, 0, 3, 0, 16, (1 << 31) - 3, 19),
     "wide20": (6, 2, 4096, 0, 20, 12, 14, 0, 6, 0, 20, 9, 20),
-    # frames > the 16 KB LDS window while k_pack32 is active: handed to k_pack by list
+    # frames > the 16 KB LDS window: with k_pack32 active (knob 2 / 7 below) handed to k_pack
+    # by list
     "big3ch_list": (8, 3, 4608, 0, 20, 12, 12, 0, 5, 0, 20, 3, 21),
     # k_packw batches: a block that is not a multiple of 8 (the row's last chunk read value by
     # value), 5-value partitions (order 11 at 10240: every frame handed to k_pack by list), and
@@ -127,11 +128,12 @@ def test_device_pointer_path_matches_host_path(az):
 
 @pytest.mark.parametrize("gen", [1, 2, 3, 7])
 @pytest.mark.parametrize("name", ["c2", "c1_tail", "bs16_3ch", "c3_stereo", "c3_tail", "wide20", "wide_odd",
-                                  "wide_fine", "wide16_tail"])
+                                  "wide_fine", "wide16_tail", "big3ch_list", "c5_fixed", "bs8_coded6"])
 def test_general_writer_alone_matches(az, name, gen):
     """Knob FLACMI_PACK_GENERIC=1 (every frame through the general k_pack) and =2 (k_packw
-    off: frames too wide for k_pack32 go to k_pack) give the default path's bytes; the c3
-    frames exercise k_packw's ring against k_pack, and =3 (k_packw with tiles of 2048
+    off: k_pack32 for the frames it fits, k_pack for the rest) give the default path's bytes
+    (k_packw for every 32-bit batch); the c3 frames exercise k_packw's ring against k_pack,
+    and =3 (k_packw with tiles of 2048
     values, about 1400 ring words for these 24-bit frames) its redo of a segment that
     overruns the 1024-word ring; =7 keeps k_pack32 on its 16 KB window (the default takes
     the 12 KB window when a verbatim frame fits it with a quarter to spare)."""
