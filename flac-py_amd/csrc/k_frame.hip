@@ -27,10 +27,11 @@
  *                  and starts from 0, so CRC(A||B) = CRC(A)*x^(8|B|) + CRC(B) mod P).
  *                  The general writer: 64-bit residuals, partitions under 8 values and
  *                  the frames the two kernels below hand over by list.
- *   k_pack32       frames that fit one LDS window (12 KB when a verbatim frame fits it,
- *                  else 16 KB): contiguous chunk runs per thread, one scan per subframe.
- *   k_packw        frames wider than k_pack32 takes (config 3): the window as a ring,
- *                  finished 2 KB chunks leaving it as the tiles advance.
+ *   k_packw        the default for 32-bit residual rows: one wave per frame, a 4 KB LDS
+ *                  ring, finished 512-byte chunks leaving it as the tiles advance.
+ *   k_pack32       (knob FLACMI_PACK_GENERIC=2) frames that fit one LDS window (12 KB when
+ *                  a verbatim frame fits it, else 16 KB): contiguous chunk runs per
+ *                  thread, one scan per subframe.
  *
  * Bit coordinates inside k_pack are "aligned": bit 0 is the MSB of the 32-bit word that
  * holds the frame's first byte, so window word k is output word (F >> 2) + wb + k.  The
