@@ -27,8 +27,9 @@
  *                  and starts from 0, so CRC(A||B) = CRC(A)*x^(8|B|) + CRC(B) mod P).
  *                  The general writer: 64-bit residuals, partitions under 8 values and
  *                  the frames the two kernels below hand over by list.
- *   k_packw        the default for 32-bit residual rows: one wave per frame, a 4 KB LDS
- *                  ring, finished 512-byte chunks leaving it as the tiles advance.
+ *   k_packw        the default for 32-bit residual rows: one wave per frame, a 2 KB (samples
+ *                  of <= 16 bits) or 4 KB LDS ring, finished 512-byte chunks leaving it as
+ *                  the tiles advance.
  *   k_pack32       (knob FLACMI_PACK_GENERIC=2) frames that fit one LDS window (12 KB when
  *                  a verbatim frame fits it, else 16 KB): contiguous chunk runs per
  *                  thread, one scan per subframe.
@@ -1360,6 +1361,13 @@ __global__ __launch_bounds__(kPackThreads) __attribute__((amdgpu_waves_per_eu(6,
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_packw128(FrameArgs a) {
     packw_frame<1, 128, 2048>(a);
 }
+/* samples of <= 16 bits: a 2 KB ring (5.2 KB of LDS: 24 workgroups a CU, the VGPR limit,
+ * instead of 21).  A 512-value tile fits it above the < 128 waiting words up to 24 bits a
+ * value; 16-bit residuals stay far below.  c2 frames 8.01 -> 7.35 ms same box (c3's 24-bit
+ * frames only 5.02 -> 4.93, with tiles near the limit: they keep the 4 KB ring). */
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_packw2k(FrameArgs a) {
+    packw_frame<1, 64, 512>(a);
+}
 
 hipError_t launch_frame_sizes(const FrameArgs& a, int64_t* bsum, hipStream_t s) {
     if (a.n_frames <= 0) return hipSuccess;
@@ -1418,6 +1426,7 @@ hipError_t launch_pack(const FrameArgs& a, hipStream_t s) {
         if (pack_generic == 3) hipLaunchKernelGGL(k_packw_redo_test, g, dim3(64), 0, s, b);
         else if (pack_generic == 6) hipLaunchKernelGGL(k_packw256, g, dim3(kPackThreads), 0, s, b);
         else if (pack_generic == 8) hipLaunchKernelGGL(k_packw128, g, dim3(128), 0, s, b);
+        else if (a.sample_size <= 16) hipLaunchKernelGGL(k_packw2k, g, dim3(64), 0, s, b);
         else hipLaunchKernelGGL(k_packw, g, dim3(64), 0, s, b);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
